@@ -1,0 +1,186 @@
+/*
+ * pdsc.h -- C ABI of libpdsc.so, the MI355X (gfx950) hot path of PointDSC.
+ *
+ * Drop-in boundary for the reference's testing-mode forward
+ * (models/PointDSC.py:128-197 of AmnonDrory/PointDSC) and the functions it
+ * calls.  Each entry point names the reference code it replaces.
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer (hipMalloc / torch CUDA
+ *     tensor storage) unless documented otherwise; all tensors are dense,
+ *     row-major, fp32 unless stated; index tensors are int32.
+ *   - B = number of independent scan pairs processed by one call (the
+ *     reference's public forward is bs == 1; B > 1 is the batched API);
+ *     N = correspondences per pair (same N for every pair of a call).
+ *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default
+ *     stream), never allocate, never synchronise, and never free caller
+ *     memory: scratch comes from a caller-allocated workspace whose size the
+ *     matching *_workspace_bytes() query returns.  All functions are
+ *     stateless and re-entrant.
+ *   - Return value: PDSC_OK or an error code; no exception crosses the ABI.
+ *     pdsc_last_error() returns a thread-local message for the last failure.
+ */
+#ifndef PDSC_H_
+#define PDSC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *pdsc_stream_t; /* hipStream_t */
+
+enum pdsc_status {
+    PDSC_OK = 0,
+    PDSC_ERR_ARG = 1,         /* bad shape / null pointer / unsupported hyper-parameter */
+    PDSC_ERR_HIP = 2,         /* a HIP runtime call failed (launch error) */
+    PDSC_ERR_UNSUPPORTED = 3, /* valid for the reference, not implemented here */
+};
+
+/* Hyper-parameters of PointDSC.__init__ (models/PointDSC.py:81-100). */
+typedef struct pdsc_config {
+    int32_t in_dim;           /* 6 */
+    int32_t num_layers;       /* 12 in both release configs */
+    int32_t num_channels;     /* 128 (the only width the HIP kernels implement) */
+    int32_t num_iterations;   /* power-iteration cap, 10 */
+    int32_t k;                /* NSM neighbourhood, 40 (clipped to N-1 per call, :250) */
+    double ratio;             /* seed ratio, 0.1: S = int(N * ratio) as Python computes it (:174) */
+    float inlier_threshold;   /* tau of :328/:335 */
+    float nms_radius;         /* R of :174 */
+    float refine_threshold;   /* :415-418: 0.10 if inlier_threshold == 0.10 else 1.2 */
+} pdsc_config;
+
+const char *pdsc_version(void);
+const char *pdsc_last_error(void);
+
+/* ---------------------------------------------------------------- weights --
+ * Packs the reference's parameters (device pointers, in the order of
+ * pdsc_param_names()) into the kernels' layout: Conv1d(k=1) weights re-tiled
+ * for 32x32x2 f32 MFMA fragments; eval BatchNorm turned into the per-channel
+ * (alpha, beta) torch-CPU uses (alpha = w / sqrt(var + 1e-5), beta = b - mean*alpha);
+ * sigma and sigma_spat copied into the blob header (read on device, no host sync).
+ * Replaces: nothing in the reference (it reads nn.Module parameters directly).
+ */
+int32_t pdsc_param_count(const pdsc_config *cfg);
+const char *pdsc_param_name(const pdsc_config *cfg, int32_t i); /* state_dict key */
+size_t pdsc_packed_weights_floats(const pdsc_config *cfg);
+int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *params_host_array,
+                          float *packed, pdsc_stream_t stream);
+
+/* ---------------------------------------------------------- a1 compat ------
+ * M[b,i,j] = max(0, 1 - (|s_i-s_j| - |t_i-t_j|)^2 / sigma_d^2), bit-exact with
+ * torch-CPU fp32.  Replaces models/PointDSC.py:150-153.  sigma_d is read on
+ * device from `sigma_d_dev` (the checkpoint's sigma_spat, :98).
+ * src,tgt [B,N,3]; M [B,N,N].                                              */
+int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N,
+                        const float *sigma_d_dev, float *M, pdsc_stream_t stream);
+
+/* -------------------------------------------------- a2-a4 encoder ----------
+ * SCNonlocal encoder + F.normalize + classification MLP.
+ * Replaces models/PointDSC.py:155-156 and :171 (NonLocalNet.forward :65-77,
+ * NonLocalBlock.forward :27-45).  corr_pos [B,N,in_dim]; M [B,N,N] (must be
+ * symmetric -- the spatial compatibility is; the attention kernel reads it
+ * column-wise).  Outputs: feat [B,N,C] (corr_features), normed [B,N,C],
+ * conf [B,N] (the classifier logits).                                        */
+size_t pdsc_encoder_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N);
+int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                         const float *M, int32_t B, int32_t N, float *feat, float *normed,
+                         float *conf, void *workspace, size_t workspace_bytes,
+                         pdsc_stream_t stream);
+
+/* The attention core of one NonLocalBlock (models/PointDSC.py:36-42) alone:
+ * msg[b,i,:] = sum_j softmax_j(M_ij * q_i.k_j / sqrt(C)) v_j, heads = 1.
+ * q,k,v [B,N,C]; msg [B,N,C].  C must be 128.                              */
+size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C);
+int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const float *M,
+                           int32_t B, int32_t N, int32_t C, float *msg, void *workspace,
+                           size_t workspace_bytes, pdsc_stream_t stream);
+
+/* The attention kernel exactly as the encoder launches it, for measurement:
+ * q/k/v are PADDED [B,Npad,C] (rows >= N zero, Npad and nsplit from
+ * pdsc_attention_layout); outputs the split partials opart [B,nsplit,Npad,C]
+ * (unnormalised) and ml [B,nsplit,Npad,2] (running max, sum).               */
+int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit);
+int32_t pdsc_attention_partials_f32(const float *q_pad, const float *k_pad, const float *v_pad,
+                                    const float *M, int32_t B, int32_t N, float *opart, float *ml,
+                                    pdsc_stream_t stream);
+
+/* ------------------------------------------------------- a5 seeds ----------
+ * pick_seeds: radius NMS on the confidences then the top-S of
+ * conf * is_local_max in descending order (ties: ascending index).
+ * Replaces models/PointDSC.py:199-217.  src [B,N,3]; conf [B,N];
+ * seeds [B,S] int32; is_local_max [B,N] (0/1 fp32, may be NULL).           */
+int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t N, float radius,
+                        int32_t S, int32_t *seeds, float *is_local_max, pdsc_stream_t stream);
+
+/* ------------------------------------------------------- a6 seed kNN -------
+ * For each seed row: the k nearest correspondences in feature space,
+ * d_j = 2 - 2 f_s.f_j, topk(k+1, smallest)[1:] -- the FIRST of the k+1
+ * (ascending distance, ascending index) is dropped positionally.
+ * Replaces models/common.py:48-69 + models/PointDSC.py:250-252 (only the
+ * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k].    */
+size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S);
+int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
+                      int32_t S, int32_t k, int32_t *knn, void *workspace, size_t workspace_bytes,
+                      pdsc_stream_t stream);
+
+/* ------------------------------------------------ a7-a8 NSM weights --------
+ * Local k x k feature x spatial consistency (diag 0), power iteration with
+ * the batch-global allclose early exit (rtol 1e-5, atol 1e-8, evaluated over
+ * all S seeds of a pair, as torch.allclose does over the bs*S batch), then
+ * w = v / (sum v + 1e-6).  Replaces models/PointDSC.py:257-282, :338-358.
+ * sigma_dev / sigma_d_dev: device scalars (learned sigma, sigma_spat).
+ * weights [B,S,k]; iters_used [B] int32 (may be NULL).                      */
+size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t S, int32_t k, int32_t num_iterations);
+int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt,
+                         const int32_t *knn, int32_t B, int32_t N, int32_t C, int32_t S, int32_t k,
+                         int32_t num_iterations, const float *sigma_dev, const float *sigma_d_dev,
+                         float *weights, int32_t *iters_used, void *workspace,
+                         size_t workspace_bytes, pdsc_stream_t stream);
+
+/* ------------------------------------------------------- a9 Kabsch ---------
+ * rigid_transform_3d: weighted centroids, H = Am^T diag(w) Bm, R from the SVD
+ * of H (3x3, fp64 Jacobi on device) with the det(V U^T) reflection fix,
+ * t = c_B - R c_A, packed as 4x4.  Replaces models/common.py:7-45 (whose SVD
+ * runs on the host CPU).  A,Bp [nb,n,3]; w [nb,n] (NULL = ones); trans [nb,4,4]. */
+int32_t pdsc_rigid_transform_3d(const float *A, const float *Bp, const float *w, int32_t nb,
+                                int32_t n, float *trans, pdsc_stream_t stream);
+
+/* --------------------------------------------- a10 verification ------------
+ * Seed hypotheses: Kabsch on each seed's kNN set with `weights`, fitness =
+ * mean(|R_s src + t_s - tgt| < tau), best = first argmax, final_labels from
+ * the best hypothesis.  Replaces models/PointDSC.py:287-335.
+ * seed_trans [B,S,4,4] and fitness [B,S] are required (they host the per-seed
+ * scratch); best [B] int32 (may be NULL); trans [B,4,4]; labels [B,N].      */
+int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *knn,
+                             const float *weights, int32_t B, int32_t N, int32_t S, int32_t k,
+                             float tau, float *seed_trans, float *fitness, int32_t *best,
+                             float *trans, float *labels, pdsc_stream_t stream);
+
+/* ------------------------------------------------ a11 post-refinement ------
+ * <= 20 IRLS re-fits on the inliers of |R src + t - tgt| < thr with weights
+ * 1/(1 + (L2/thr)^2), stopping when the inlier count repeats.  Device-side
+ * loop, one workgroup per pair.  Replaces models/PointDSC.py:403-438.
+ * trans [B,4,4] in/out.                                                      */
+int32_t pdsc_post_refine(float *trans, const float *src, const float *tgt, int32_t B, int32_t N,
+                         float thr, pdsc_stream_t stream);
+
+/* ----------------------------------------------- full testing forward ------
+ * PointDSC.forward(data) with 'testing' in data (models/PointDSC.py:128-197)
+ * for B independent pairs: compat -> encoder -> classifier -> seeds -> kNN ->
+ * NSM -> hypotheses -> post-refinement.  corr_pos [B,N,in_dim];
+ * src,tgt [B,N,3]; final_trans [B,4,4]; final_labels [B,N].
+ * Optional debug outputs (NULL to skip): conf [B,N], seeds [B,S].           */
+size_t pdsc_forward_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N);
+int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                             const float *src, const float *tgt, int32_t B, int32_t N,
+                             float *final_trans, float *final_labels, float *conf_out,
+                             int32_t *seeds_out, void *workspace, size_t workspace_bytes,
+                             pdsc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDSC_H_ */

@@ -1,0 +1,107 @@
+"""ctypes binding of ``libpdsc.so`` (the C ABI declared in ``include/pdsc.h``).
+
+The library is built in-tree by ``make -C pointdsc_amd/csrc`` (or
+``__graft_entry__.build()``).  There is no fallback: if the library is missing
+or cannot be loaded, every entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpdsc.so")
+
+c_int32, c_size_t, c_float, c_double = ctypes.c_int32, ctypes.c_size_t, ctypes.c_float, ctypes.c_double
+vp = ctypes.c_void_p
+
+
+class PdscConfig(ctypes.Structure):
+    """``struct pdsc_config`` (include/pdsc.h)."""
+    _fields_ = [
+        ("in_dim", c_int32),
+        ("num_layers", c_int32),
+        ("num_channels", c_int32),
+        ("num_iterations", c_int32),
+        ("k", c_int32),
+        ("ratio", c_double),
+        ("inlier_threshold", c_float),
+        ("nms_radius", c_float),
+        ("refine_threshold", c_float),
+    ]
+
+
+CFG = ctypes.POINTER(PdscConfig)
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "pdsc_version": (ctypes.c_char_p, []),
+    "pdsc_last_error": (ctypes.c_char_p, []),
+    "pdsc_param_count": (c_int32, [CFG]),
+    "pdsc_param_name": (ctypes.c_char_p, [CFG, c_int32]),
+    "pdsc_packed_weights_floats": (c_size_t, [CFG]),
+    "pdsc_pack_weights": (c_int32, [CFG, ctypes.POINTER(vp), vp, vp]),
+    "pdsc_compat_f32": (c_int32, [vp, vp, c_int32, c_int32, vp, vp, vp]),
+    "pdsc_encoder_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
+    "pdsc_encoder_f32": (c_int32, [CFG, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_attention_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "pdsc_attention_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
+    "pdsc_attention_layout": (c_int32, [c_int32, c_int32, ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)]),
+    "pdsc_attention_partials_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp]),
+    "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
+    "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+    "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
+    "pdsc_nsm_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
+    "pdsc_nsm_weights": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                   vp, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_rigid_transform_3d": (c_int32, [vp, vp, vp, c_int32, c_int32, vp, vp]),
+    "pdsc_seed_hypotheses": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_float,
+                                       vp, vp, vp, vp, vp, vp]),
+    "pdsc_post_refine": (c_int32, [vp, vp, vp, c_int32, c_int32, c_float, vp]),
+    "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
+    "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
+                                       c_size_t, vp]),
+}
+
+EXPORTS = tuple(_PROTOS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libpdsc.so once; raise RuntimeError (no fallback) if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"pointdsc_amd: HIP library {LIB_PATH} is missing; build it with "
+                    "`make -C pointdsc_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`. "
+                    "There is no CPU fallback.")
+            try:
+                lib = ctypes.CDLL(LIB_PATH)
+            except OSError as e:
+                raise RuntimeError(f"pointdsc_amd: cannot load {LIB_PATH}: {e}") from e
+            for name, (res, args) in _PROTOS.items():
+                fn = getattr(lib, name)
+                fn.restype, fn.argtypes = res, args
+            _lib = lib
+    return _lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().pdsc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def make_config(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, k=40, ratio=0.1,
+                inlier_threshold=0.10, nms_radius=0.10) -> PdscConfig:
+    """Build ``pdsc_config``; the refine threshold follows models/PointDSC.py:415-418."""
+    refine = 0.10 if inlier_threshold == 0.10 else 1.2
+    return PdscConfig(int(in_dim), int(num_layers), int(num_channels), int(num_iterations), int(k),
+                      float(ratio), float(inlier_threshold), float(nms_radius), float(refine))

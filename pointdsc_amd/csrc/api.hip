@@ -1,0 +1,479 @@
+// api.hip -- the C ABI of libpdsc.so (declared in include/pdsc.h).
+//
+// Host-side orchestration only: argument checks, workspace carving and kernel
+// launches on the caller's stream.  No allocation, no synchronisation.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "pdsc_internal.hpp"
+
+using namespace pdsc;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local std::string g_name;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(PDSC_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+hipStream_t S_(pdsc_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Bump allocator over a caller workspace (256-B aligned slices).
+struct Carve {
+    char *base;
+    size_t off = 0;
+    explicit Carve(void *p) : base(static_cast<char *>(p)) {}
+    template <typename T> T *take(size_t n) {
+        T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+        off += align_bytes(n * sizeof(T));
+        return p;
+    }
+};
+
+int check_cfg(const pdsc_config *cfg) {
+    if (!cfg) return fail(PDSC_ERR_ARG, "cfg is NULL");
+    if (cfg->num_channels != CH)
+        return fail(PDSC_ERR_UNSUPPORTED, "num_channels=%d: only %d is implemented", cfg->num_channels, CH);
+    if (cfg->num_layers < 1 || cfg->num_layers > 64)
+        return fail(PDSC_ERR_UNSUPPORTED, "num_layers=%d not in [1, 64]", cfg->num_layers);
+    if (cfg->in_dim < 1 || cfg->in_dim > 64) return fail(PDSC_ERR_UNSUPPORTED, "in_dim=%d", cfg->in_dim);
+    if (cfg->num_iterations < 0 || cfg->num_iterations > 31)
+        return fail(PDSC_ERR_UNSUPPORTED, "num_iterations=%d not in [0, 31]", cfg->num_iterations);
+    if (cfg->k < 1) return fail(PDSC_ERR_ARG, "k=%d", cfg->k);
+    return PDSC_OK;
+}
+
+struct Dims {
+    int B, N, Npad, S, k, T, nsplit;
+};
+
+int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
+    if (B < 1 || N < 2) return fail(PDSC_ERR_ARG, "B=%d N=%d (need B >= 1, N >= 2)", B, N);
+    d.B = B;
+    d.N = N;
+    d.Npad = round_up(N, QB);
+    d.S = (int)((double)N * cfg->ratio);  // int(num_corr * self.ratio) (:174)
+    d.k = std::min(cfg->k, N - 1);        // (:250)
+    d.T = cfg->num_iterations;
+    d.nsplit = attention_nsplit(B, N);
+    if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
+    if (d.k > 64) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 64", d.k);
+    return PDSC_OK;
+}
+
+struct EncBufs {
+    float *feat, *q, *k, *v, *opart, *ml;
+};
+
+EncBufs carve_encoder(Carve &c, const Dims &d) {
+    EncBufs e;
+    const size_t rows = (size_t)d.B * d.Npad * CH;
+    e.feat = c.take<float>(rows);
+    e.q = c.take<float>(rows);
+    e.k = c.take<float>(rows);
+    e.v = c.take<float>(rows);
+    e.opart = c.take<float>(rows * d.nsplit);
+    e.ml = c.take<float>((size_t)d.B * d.Npad * d.nsplit * 2);
+    return e;
+}
+
+int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
+                const Dims &d, const EncBufs &e, float *feat_out, float *normed, float *conf,
+                hipStream_t s) {
+    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
+    for (int l = 0; l < lay.L; ++l) {
+        HIPCHK(launch_attention(e.q, e.k, e.v, M, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        if (l + 1 < lay.L)
+            HIPCHK(launch_pw_mid(packed, lay, l, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
+                                 e.k, e.v, s));
+        else
+            HIPCHK(launch_pw_last(packed, lay, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
+                                  feat_out, normed, conf, s));
+    }
+    return PDSC_OK;
+}
+
+struct NsmBufs {
+    float *hist, *weights;
+    unsigned *mask;
+};
+
+NsmBufs carve_nsm(Carve &c, int B, int S, int k, int T) {
+    NsmBufs n;
+    n.hist = c.take<float>((size_t)B * S * std::max(T, 1) * k);
+    n.mask = c.take<unsigned>((size_t)B);
+    n.weights = c.take<float>((size_t)B * S * k);
+    return n;
+}
+
+int run_nsm(const float *normed, const float *src, const float *tgt, const int *knn, int B, int N,
+            int S, int k, int T, const float *sigma, const float *sigma_d, const NsmBufs &nb,
+            float *weights, int *iters, hipStream_t s) {
+    HIPCHK(hipMemsetAsync(nb.mask, 0xff, sizeof(unsigned) * B, s));
+    if (T > 0)
+        HIPCHK(launch_nsm_power(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
+    HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, weights, iters, s));
+    return PDSC_OK;
+}
+
+struct FwdBufs {
+    float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights;
+    int *seeds, *knn, *counts;
+    EncBufs enc;
+    NsmBufs nsm;
+};
+
+FwdBufs carve_forward(Carve &c, const Dims &d) {
+    FwdBufs f;
+    f.M = c.take<float>((size_t)d.B * d.N * d.N);
+    f.enc = carve_encoder(c, d);
+    f.normed = c.take<float>((size_t)d.B * d.N * CH);
+    f.conf = c.take<float>((size_t)d.B * d.N);
+    f.lm = c.take<float>((size_t)d.B * d.N);
+    f.seeds = c.take<int>((size_t)d.B * d.S);
+    f.kdist = c.take<float>((size_t)d.B * d.S * d.N);
+    f.knn = c.take<int>((size_t)d.B * d.S * d.k);
+    f.nsm = carve_nsm(c, d.B, d.S, d.k, d.T);
+    f.weights = f.nsm.weights;
+    f.seed_trans = c.take<float>((size_t)d.B * d.S * 16);
+    f.counts = c.take<int>((size_t)d.B * d.S);
+    return f;
+}
+
+int need_ws(size_t have, size_t need) {
+    if (have < need) return fail(PDSC_ERR_ARG, "workspace too small: %zu < %zu bytes", have, need);
+    return PDSC_OK;
+}
+
+}  // namespace
+
+#define RET_IF(x)                  \
+    do {                           \
+        int r_ = (x);              \
+        if (r_ != PDSC_OK) return r_; \
+    } while (0)
+
+extern "C" {
+
+const char *pdsc_version(void) { return "pdsc 0.1.0 gfx950"; }
+const char *pdsc_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------ weights
+int32_t pdsc_param_count(const pdsc_config *cfg) { return cfg ? 10 + 26 * cfg->num_layers : -1; }
+
+const char *pdsc_param_name(const pdsc_config *cfg, int32_t i) {
+    if (!cfg || i < 0 || i >= pdsc_param_count(cfg)) return nullptr;
+    static const char *bn[] = {"weight", "bias", "running_mean", "running_var"};
+    static const char *per[] = {"fc_message.0.weight", "fc_message.0.bias", "fc_message.1.weight",
+                                "fc_message.1.bias", "fc_message.1.running_mean", "fc_message.1.running_var",
+                                "fc_message.3.weight", "fc_message.3.bias", "fc_message.4.weight",
+                                "fc_message.4.bias", "fc_message.4.running_mean", "fc_message.4.running_var",
+                                "fc_message.6.weight", "fc_message.6.bias", "projection_q.weight",
+                                "projection_q.bias", "projection_k.weight", "projection_k.bias",
+                                "projection_v.weight", "projection_v.bias"};
+    static const char *tail[] = {"encoder.layer0.weight", "encoder.layer0.bias", "classification.0.weight",
+                                 "classification.0.bias", "classification.2.weight", "classification.2.bias",
+                                 "classification.4.weight", "classification.4.bias"};
+    const int L = cfg->num_layers;
+    if (i == 0) return "sigma";
+    if (i == 1) return "sigma_spat";
+    i -= 2;
+    if (i < 26 * L) {
+        const int l = i / 26, o = i % 26;
+        char buf[128];
+        if (o < 2)
+            snprintf(buf, sizeof(buf), "encoder.blocks.PointCN_layer_%d.0.%s", l, o == 0 ? "weight" : "bias");
+        else if (o < 6)
+            snprintf(buf, sizeof(buf), "encoder.blocks.PointCN_layer_%d.1.%s", l, bn[o - 2]);
+        else
+            snprintf(buf, sizeof(buf), "encoder.blocks.NonLocal_layer_%d.%s", l, per[o - 6]);
+        g_name = buf;
+        return g_name.c_str();
+    }
+    return tail[i - 26 * L];
+}
+
+size_t pdsc_packed_weights_floats(const pdsc_config *cfg) {
+    if (check_cfg(cfg) != PDSC_OK) return 0;
+    return make_layout(cfg->num_layers, cfg->in_dim).total;
+}
+
+int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *P, float *packed,
+                          pdsc_stream_t stream) {
+    RET_IF(check_cfg(cfg));
+    if (!P || !packed) return fail(PDSC_ERR_ARG, "null params/packed");
+    const int n = pdsc_param_count(cfg);
+    for (int i = 0; i < n; ++i)
+        if (!P[i]) return fail(PDSC_ERR_ARG, "param %d (%s) is NULL", i, pdsc_param_name(cfg, i));
+    hipStream_t s = S_(stream);
+    const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
+    HIPCHK(hipMemsetAsync(packed, 0, lay.total * sizeof(float), s));
+    HIPCHK(launch_copy(P[0], packed + lay.sigma, 1, s));
+    HIPCHK(launch_copy(P[1], packed + lay.sigma_d, 1, s));
+    auto dense = [&](const DenseOff &o, int wi, int in, int out, bool has_bn) -> hipError_t {
+        return launch_pack_dense(P[wi], P[wi + 1], has_bn ? P[wi + 2] : nullptr,
+                                 has_bn ? P[wi + 3] : nullptr, has_bn ? P[wi + 4] : nullptr,
+                                 has_bn ? P[wi + 5] : nullptr, in, out, packed + o.w, packed + o.bias,
+                                 packed + o.alpha, packed + o.beta, s);
+    };
+    for (int l = 0; l < cfg->num_layers; ++l) {
+        const int b = 2 + 26 * l;
+        const LayerOff &lo = lay.layer[l];
+        HIPCHK(dense(lo.pcn, b + 0, CH, CH, true));
+        HIPCHK(dense(lo.fc0, b + 6, CH, CH2, true));
+        HIPCHK(dense(lo.fc3, b + 12, CH2, CH2, true));
+        HIPCHK(dense(lo.fc6, b + 18, CH2, CH, false));
+        HIPCHK(dense(lo.q, b + 20, CH, CH, false));
+        HIPCHK(dense(lo.k, b + 22, CH, CH, false));
+        HIPCHK(dense(lo.v, b + 24, CH, CH, false));
+    }
+    const int t = 2 + 26 * cfg->num_layers;
+    HIPCHK(launch_copy(P[t], packed + lay.l0_w, CH * cfg->in_dim, s));
+    HIPCHK(launch_copy(P[t + 1], packed + lay.l0_b, CH, s));
+    HIPCHK(dense(lay.c0, t + 2, CH, CLS, false));
+    HIPCHK(dense(lay.c2, t + 4, CLS, CLS, false));
+    HIPCHK(launch_copy(P[t + 6], packed + lay.c4_w, CLS, s));
+    HIPCHK(launch_copy(P[t + 7], packed + lay.c4_b, 1, s));
+    return PDSC_OK;
+}
+
+// ------------------------------------------------------------------- a1
+int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N,
+                        const float *sigma_d_dev, float *M, pdsc_stream_t stream) {
+    if (!src || !tgt || !sigma_d_dev || !M) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    HIPCHK(launch_compat(src, tgt, B, N, sigma_d_dev, M, S_(stream)));
+    return PDSC_OK;
+}
+
+// ---------------------------------------------------------------- a2-a4
+size_t pdsc_encoder_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N) {
+    Dims d;
+    if (check_cfg(cfg) != PDSC_OK || make_dims(cfg, B, N, d) != PDSC_OK) return 0;
+    Carve c(nullptr);
+    carve_encoder(c, d);
+    return c.off;
+}
+
+int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                         const float *M, int32_t B, int32_t N, float *feat, float *normed, float *conf,
+                         void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cfg(cfg));
+    Dims d;
+    RET_IF(make_dims(cfg, B, N, d));
+    if (!packed || !corr_pos || !M || !normed || !conf || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_encoder_workspace_bytes(cfg, B, N)));
+    Carve c(ws);
+    const EncBufs e = carve_encoder(c, d);
+    const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
+    return run_encoder(lay, packed, corr_pos, M, d, e, feat, normed, conf, S_(stream));
+}
+
+size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
+    if (C != CH || B < 1 || N < 1) return 0;
+    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
+    Carve c(nullptr);
+    for (int i = 0; i < 3; ++i) c.take<float>((size_t)B * Npad * CH);
+    c.take<float>((size_t)B * Npad * CH * ns);
+    c.take<float>((size_t)B * Npad * ns * 2);
+    return c.off;
+}
+
+int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const float *M, int32_t B,
+                           int32_t N, int32_t C, float *msg, void *ws, size_t ws_bytes,
+                           pdsc_stream_t stream) {
+    if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
+    if (!q || !k || !v || !M || !msg || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    RET_IF(need_ws(ws_bytes, pdsc_attention_workspace_bytes(B, N, C)));
+    hipStream_t s = S_(stream);
+    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
+    Carve c(ws);
+    float *qp = c.take<float>((size_t)B * Npad * CH);
+    float *kp = c.take<float>((size_t)B * Npad * CH);
+    float *vp = c.take<float>((size_t)B * Npad * CH);
+    float *op = c.take<float>((size_t)B * Npad * CH * ns);
+    float *ml = c.take<float>((size_t)B * Npad * ns * 2);
+    // re-pad the caller's [B][N][C] rows to the kernel's [B][Npad][C] (zero rows)
+    const size_t pad_bytes = (size_t)B * Npad * CH * sizeof(float);
+    for (float *p : {qp, kp, vp}) HIPCHK(hipMemsetAsync(p, 0, pad_bytes, s));
+    const size_t row = CH * sizeof(float);
+    HIPCHK(hipMemcpy2DAsync(qp, Npad * row, q, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpy2DAsync(kp, Npad * row, k, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpy2DAsync(vp, Npad * row, v, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
+    HIPCHK(launch_attention(qp, kp, vp, M, B, N, Npad, ns, op, ml, s));
+    HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
+    return PDSC_OK;
+}
+
+int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit) {
+    if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    *Npad = round_up(N, QB);
+    *nsplit = attention_nsplit(B, N);
+    return PDSC_OK;
+}
+
+int32_t pdsc_attention_partials_f32(const float *q, const float *k, const float *v, const float *M,
+                                    int32_t B, int32_t N, float *opart, float *ml, pdsc_stream_t stream) {
+    if (!q || !k || !v || !M || !opart || !ml) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    HIPCHK(launch_attention(q, k, v, M, B, N, round_up(N, QB), attention_nsplit(B, N), opart, ml,
+                            S_(stream)));
+    return PDSC_OK;
+}
+
+// -------------------------------------------------------------------- a5
+int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t N, float radius,
+                        int32_t S, int32_t *seeds, float *is_local_max, pdsc_stream_t stream) {
+    if (!src || !conf || !seeds || !is_local_max) return fail(PDSC_ERR_ARG, "null pointer (is_local_max is used as scratch)");
+    if (B < 1 || N < 1 || S < 1 || S > N) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d", B, N, S);
+    hipStream_t s = S_(stream);
+    HIPCHK(launch_local_max(src, conf, B, N, radius, is_local_max, s));
+    HIPCHK(launch_seed_rank(conf, is_local_max, B, N, S, seeds, s));
+    return PDSC_OK;
+}
+
+// -------------------------------------------------------------------- a6
+size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S) {
+    return align_bytes((size_t)B * S * N * sizeof(float));
+}
+
+int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
+                      int32_t S, int32_t k, int32_t *knn, void *ws, size_t ws_bytes,
+                      pdsc_stream_t stream) {
+    if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
+    if (!normed || !seeds || !knn || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || S < 1 || k < 1 || k + 1 > N || k > 255) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
+    RET_IF(need_ws(ws_bytes, pdsc_seed_knn_workspace_bytes(B, N, S)));
+    hipStream_t s = S_(stream);
+    float *dist = static_cast<float *>(ws);
+    HIPCHK(launch_knn_dist(normed, seeds, B, N, S, dist, s));
+    HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
+    return PDSC_OK;
+}
+
+// ----------------------------------------------------------------- a7-a8
+size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t S, int32_t k, int32_t T) {
+    Carve c(nullptr);
+    carve_nsm(c, B, S, k, T);
+    return c.off;
+}
+
+int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt, const int32_t *knn,
+                         int32_t B, int32_t N, int32_t C, int32_t S, int32_t k, int32_t T,
+                         const float *sigma, const float *sigma_d, float *weights, int32_t *iters,
+                         void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
+    if (!normed || !src || !tgt || !knn || !sigma || !sigma_d || !weights || !ws)
+        return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || S < 1 || k < 1 || k > 64 || T < 0 || T > 31) return fail(PDSC_ERR_ARG, "B=%d S=%d k=%d T=%d", B, S, k, T);
+    RET_IF(need_ws(ws_bytes, pdsc_nsm_workspace_bytes(B, S, k, T)));
+    Carve c(ws);
+    NsmBufs nb = carve_nsm(c, B, S, k, T);
+    return run_nsm(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb, weights, iters, S_(stream));
+}
+
+// -------------------------------------------------------------------- a9
+int32_t pdsc_rigid_transform_3d(const float *A, const float *Bp, const float *w, int32_t nb, int32_t n,
+                                float *trans, pdsc_stream_t stream) {
+    if (!A || !Bp || !trans) return fail(PDSC_ERR_ARG, "null pointer");
+    if (nb < 1 || n < 0) return fail(PDSC_ERR_ARG, "nb=%d n=%d", nb, n);
+    HIPCHK(launch_rigid(A, Bp, w, nb, n, trans, S_(stream)));
+    return PDSC_OK;
+}
+
+// ------------------------------------------------------------------- a10
+int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *knn, const float *weights,
+                             int32_t B, int32_t N, int32_t S, int32_t k, float tau, float *seed_trans,
+                             float *fitness, int32_t *best, float *trans, float *labels,
+                             pdsc_stream_t stream) {
+    if (!src || !tgt || !knn || !weights || !trans || !labels || !seed_trans)
+        return fail(PDSC_ERR_ARG, "null pointer (seed_trans is required as scratch)");
+    if (B < 1 || N < 1 || S < 1 || k < 1 || k > 64) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
+    hipStream_t s = S_(stream);
+    // the integer inlier counts live in the caller's fitness buffer until select_best turns
+    // each into count / N (same thread, same element)
+    if (!fitness) return fail(PDSC_ERR_ARG, "fitness [B,S] buffer is required (hosts the inlier counts)");
+    int *counts = reinterpret_cast<int *>(fitness);
+    HIPCHK(launch_hypotheses(src, tgt, knn, weights, B, N, S, k, tau, seed_trans, counts, s));
+    HIPCHK(launch_select_best(src, tgt, seed_trans, counts, B, N, S, tau, fitness, best, trans, labels, s));
+    return PDSC_OK;
+}
+
+// ------------------------------------------------------------------- a11
+int32_t pdsc_post_refine(float *trans, const float *src, const float *tgt, int32_t B, int32_t N, float thr,
+                         pdsc_stream_t stream) {
+    if (!trans || !src || !tgt) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    HIPCHK(launch_post_refine(trans, src, tgt, B, N, thr, S_(stream)));
+    return PDSC_OK;
+}
+
+// --------------------------------------------------------------- forward
+size_t pdsc_forward_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N) {
+    Dims d;
+    if (check_cfg(cfg) != PDSC_OK || make_dims(cfg, B, N, d) != PDSC_OK) return 0;
+    Carve c(nullptr);
+    carve_forward(c, d);
+    return c.off;
+}
+
+int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                             const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
+                             float *final_labels, float *conf_out, int32_t *seeds_out, void *ws,
+                             size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cfg(cfg));
+    Dims d;
+    RET_IF(make_dims(cfg, B, N, d));
+    if (!packed || !corr_pos || !src || !tgt || !final_trans || !final_labels || !ws)
+        return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_forward_workspace_bytes(cfg, B, N)));
+    hipStream_t s = S_(stream);
+    Carve c(ws);
+    const FwdBufs f = carve_forward(c, d);
+    const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
+    const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
+    // a1 (:150-153)
+    HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    // a2-a4 (:155-156, :171)
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, d, f.enc, nullptr, f.normed, f.conf, s));
+    // a5 (:174)
+    HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s));
+    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
+    // a6 (:250-252)
+    HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
+    HIPCHK(launch_knn_dist(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
+    // a7-a8 (:257-282)
+    RET_IF(run_nsm(f.normed, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
+                   nullptr, s));
+    // a9-a10 (:287-335)
+    HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
+                             f.seed_trans, f.counts, s));
+    HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
+                              nullptr, nullptr, final_trans, final_labels, s));
+    // a11 (:186, :403-438)
+    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s));
+    if (conf_out) HIPCHK(hipMemcpyAsync(conf_out, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
+    if (seeds_out)
+        HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    return PDSC_OK;
+}
+
+}  // extern "C"

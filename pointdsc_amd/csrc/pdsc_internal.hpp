@@ -1,0 +1,142 @@
+// pdsc_internal.hpp -- launchers and packed-weight layout shared by the
+// translation units of libpdsc (not part of the C ABI).
+#pragma once
+#include "pdsc_common.hpp"
+#include "../../include/pdsc.h"
+
+namespace pdsc {
+
+constexpr int CH = 128;       // num_channels implemented by the MFMA kernels
+constexpr int CH2 = CH / 2;   // fc_message hidden width (models/PointDSC.py:12-20)
+constexpr int CLS = 32;       // classifier hidden width (models/PointDSC.py:107-113)
+constexpr int QB = 128;       // queries per attention workgroup (4 waves x 32)
+constexpr int KT = 32;        // keys per attention tile
+constexpr int PT = 32;        // points per pointwise workgroup
+
+inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
+
+// ---- packed weights --------------------------------------------------------
+// A "dense" layer (Conv1d k=1 [+BN] [+ReLU]) is stored as
+//   W  : OUT*IN floats in MFMA fragment order:
+//        Wpk[((jt*(IN/8) + g)*64 + lane)*4 + e] = W[jt*32 + (lane&31)][(lane>>5)*(IN/2) + 4g + e]
+//   bias[OUT], alpha[OUT], beta[OUT]   (alpha=1, beta=0 when no BN)
+struct DenseOff {
+    size_t w, bias, alpha, beta;
+};
+inline size_t dense_floats(int in, int out) { return (size_t)out * in + 3 * (size_t)out; }
+
+struct LayerOff {
+    DenseOff pcn, fc0, fc3, fc6, q, k, v;
+};
+
+struct PackLayout {
+    int L, in_dim;
+    size_t sigma, sigma_d;    // header scalars
+    size_t l0_w, l0_b;        // layer0 plain [CH][in_dim], bias[CH]
+    size_t cls0, cls2;        // DenseOff base of the two classifier dense layers
+    DenseOff c0, c2;
+    size_t c4_w, c4_b;        // plain [CLS], [1]
+    size_t total;
+    LayerOff layer[64];
+};
+
+inline DenseOff dense_at(size_t &o, int in, int out) {
+    DenseOff d;
+    d.w = o;
+    o += (size_t)out * in;
+    d.bias = o;
+    o += out;
+    d.alpha = o;
+    o += out;
+    d.beta = o;
+    o += out;
+    o = (o + 3) & ~size_t(3);
+    return d;
+}
+
+inline PackLayout make_layout(int L, int in_dim) {
+    PackLayout p{};
+    p.L = L;
+    p.in_dim = in_dim;
+    size_t o = 0;
+    p.sigma = 0;
+    p.sigma_d = 1;
+    o = 16;
+    p.l0_w = o;
+    o += (size_t)CH * in_dim;
+    p.l0_b = o;
+    o += CH;
+    o = (o + 3) & ~size_t(3);
+    for (int l = 0; l < L; ++l) {
+        LayerOff &lo = p.layer[l];
+        lo.pcn = dense_at(o, CH, CH);
+        lo.fc0 = dense_at(o, CH, CH2);
+        lo.fc3 = dense_at(o, CH2, CH2);
+        lo.fc6 = dense_at(o, CH2, CH);
+        lo.q = dense_at(o, CH, CH);
+        lo.k = dense_at(o, CH, CH);
+        lo.v = dense_at(o, CH, CH);
+    }
+    p.c0 = dense_at(o, CH, CLS);
+    p.c2 = dense_at(o, CLS, CLS);
+    p.c4_w = o;
+    o += CLS;
+    p.c4_b = o;
+    o += 4;
+    p.total = o;
+    return p;
+}
+
+// ---- launchers --------------------------------------------------------------
+hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
+                         float *M, hipStream_t s);
+
+hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
+                             const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
+                             float *dst_b, float *dst_a, float *dst_beta, hipStream_t s);
+hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
+
+// Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
+int attention_nsplit(int B, int N);
+hipError_t launch_attention(const float *q, const float *k, const float *v, const float *M, int B,
+                            int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s);
+// Combine partials -> msg [B][Npad][CH] (used by the standalone attention API).
+hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
+                               int nsplit, float *msg, hipStream_t s);
+
+// Pointwise chains (one workgroup per PT points).
+hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
+                           int N, int Npad, float *feat, float *q, float *k, float *v, hipStream_t s);
+hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
+                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, float *q,
+                         float *k, float *v, hipStream_t s);
+hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
+                          const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
+                          float *feat_out, float *normed, float *conf, hipStream_t s);
+
+hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
+                            float *lm, hipStream_t s);
+hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
+                            hipStream_t s);
+
+hipError_t launch_knn_dist(const float *normed, const int *seeds, int B, int N, int S, float *dist,
+                           hipStream_t s);
+hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s);
+hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
+                            int B, int N, int S, int k, int T, const float *sigma,
+                            const float *sigma_d, float *hist, unsigned *pair_mask, hipStream_t s);
+hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B, int S, int k, int T,
+                             float *weights, int *iters_used, hipStream_t s);
+hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
+                             int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
+                             hipStream_t s);
+hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
+                              const int *counts, int B, int N, int S, float tau, float *fitness,
+                              int *best, float *trans, float *labels, hipStream_t s);
+hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
+                              hipStream_t s);
+hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
+                        hipStream_t s);
+
+}  // namespace pdsc

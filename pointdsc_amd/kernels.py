@@ -1,0 +1,244 @@
+"""torch-facing wrappers of the libpdsc C ABI (one function per hot-path op).
+
+Tensors must live on a HIP device (``torch.device('cuda')`` on ROCm); every
+call runs the hand-written gfx950 kernels on torch's current stream.  There is
+no CPU or eager-PyTorch fallback: a CPU tensor or a missing library raises.
+Index outputs are int32 (the C ABI's index type).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+CH = 128
+
+
+def _dev(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} is on {t.device}: the pointdsc_amd HIP path needs device tensors "
+                           "(there is no CPU fallback)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+# --------------------------------------------------------------------- a1
+def compat(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch.Tensor:
+    """M [B,N,N] (models/PointDSC.py:150-153).  src/tgt [B,N,3]; sigma_d: device scalar tensor."""
+    src, tgt = _dev(src, "src"), _dev(tgt, "tgt")
+    sigma_d = _dev(sigma_d.reshape(-1), "sigma_d")
+    B, N, _ = src.shape
+    M = torch.empty((B, N, N), dtype=torch.float32, device=src.device)
+    check(_lib.load().pdsc_compat_f32(_p(src), _p(tgt), B, N, _p(sigma_d), _p(M), _stream(src.device)),
+          "pdsc_compat_f32")
+    return M
+
+
+# ------------------------------------------------------------------ weights
+def pack_weights(cfg: _lib.PdscConfig, named: dict) -> torch.Tensor:
+    """Pack reference state-dict tensors (on device) into the kernels' blob."""
+    L = _lib.load()
+    n = L.pdsc_param_count(ctypes.byref(cfg))
+    tensors, ptrs = [], (ctypes.c_void_p * n)()
+    device = None
+    for i in range(n):
+        key = L.pdsc_param_name(ctypes.byref(cfg), i).decode()
+        if key not in named:
+            raise KeyError(f"missing parameter {key}")
+        t = _dev(named[key].detach(), key)
+        device = t.device
+        tensors.append(t)
+        ptrs[i] = t.data_ptr()
+    packed = torch.empty(L.pdsc_packed_weights_floats(ctypes.byref(cfg)), dtype=torch.float32,
+                         device=device)
+    check(L.pdsc_pack_weights(ctypes.byref(cfg), ptrs, _p(packed), _stream(device)), "pdsc_pack_weights")
+    torch.cuda.current_stream(device).synchronize()  # keep `tensors` alive until the copies ran
+    return packed
+
+
+# ------------------------------------------------------------------- a2-a4
+def encoder(cfg, packed, corr_pos, M, want_features=True):
+    """(corr_features [B,N,C] | None, normed [B,N,C], confidence [B,N])."""
+    corr_pos, M = _dev(corr_pos, "corr_pos"), _dev(M, "M")
+    B, N, _ = corr_pos.shape
+    dev = corr_pos.device
+    L = _lib.load()
+    nb = L.pdsc_encoder_workspace_bytes(ctypes.byref(cfg), B, N)
+    ws = _workspace(nb, dev)
+    feat = torch.empty((B, N, CH), dtype=torch.float32, device=dev) if want_features else None
+    normed = torch.empty((B, N, CH), dtype=torch.float32, device=dev)
+    conf = torch.empty((B, N), dtype=torch.float32, device=dev)
+    check(L.pdsc_encoder_f32(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(M), B, N, _p(feat),
+                             _p(normed), _p(conf), _p(ws), nb, _stream(dev)), "pdsc_encoder_f32")
+    return feat, normed, conf
+
+
+def attention(q, k, v, M):
+    """softmax_j(M_ij q_i.k_j / sqrt(C)) v_j  (models/PointDSC.py:36-42); q,k,v [B,N,128]."""
+    q, k, v, M = (_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (M, "M")))
+    B, N, C = q.shape
+    L = _lib.load()
+    nb = L.pdsc_attention_workspace_bytes(B, N, C)
+    ws = _workspace(nb, q.device)
+    msg = torch.empty_like(q)
+    check(L.pdsc_attention_f32(_p(q), _p(k), _p(v), _p(M), B, N, C, _p(msg), _p(ws), nb,
+                               _stream(q.device)), "pdsc_attention_f32")
+    return msg
+
+
+# ---------------------------------------------------------------------- a5
+def pick_seeds(src, conf, radius: float, max_num: int):
+    """(seeds int32 [B,S], is_local_max [B,N]) (models/PointDSC.py:199-217)."""
+    src, conf = _dev(src, "src"), _dev(conf, "conf")
+    B, N = conf.shape
+    seeds = torch.empty((B, max_num), dtype=torch.int32, device=src.device)
+    lm = torch.empty((B, N), dtype=torch.float32, device=src.device)
+    check(_lib.load().pdsc_pick_seeds(_p(src), _p(conf), B, N, float(radius), int(max_num), _p(seeds),
+                                      _p(lm), _stream(src.device)), "pdsc_pick_seeds")
+    return seeds, lm
+
+
+# ---------------------------------------------------------------------- a6
+def seed_knn(normed, seeds, k: int):
+    """knn indices [B,S,k] int32 of the seed rows (models/common.py:48-69)."""
+    normed, seeds = _dev(normed, "normed"), _dev(seeds, "seeds", torch.int32)
+    B, N, C = normed.shape
+    S = seeds.shape[1]
+    L = _lib.load()
+    nb = L.pdsc_seed_knn_workspace_bytes(B, N, S)
+    ws = _workspace(nb, normed.device)
+    out = torch.empty((B, S, k), dtype=torch.int32, device=normed.device)
+    check(L.pdsc_seed_knn(_p(normed), _p(seeds), B, N, C, S, int(k), _p(out), _p(ws), nb,
+                          _stream(normed.device)), "pdsc_seed_knn")
+    return out
+
+
+# ------------------------------------------------------------------- a7-a8
+def nsm_weights(normed, src, tgt, knn, num_iterations, sigma, sigma_d):
+    """(weights [B,S,k], iterations used [B]) (models/PointDSC.py:257-282, :338-358)."""
+    normed, src, tgt = _dev(normed, "normed"), _dev(src, "src"), _dev(tgt, "tgt")
+    knn = _dev(knn, "knn", torch.int32)
+    sigma, sigma_d = _dev(sigma.reshape(-1), "sigma"), _dev(sigma_d.reshape(-1), "sigma_d")
+    B, N, C = normed.shape
+    _, S, k = knn.shape
+    L = _lib.load()
+    nb = L.pdsc_nsm_workspace_bytes(B, S, k, int(num_iterations))
+    ws = _workspace(nb, normed.device)
+    w = torch.empty((B, S, k), dtype=torch.float32, device=normed.device)
+    it = torch.empty((B,), dtype=torch.int32, device=normed.device)
+    check(L.pdsc_nsm_weights(_p(normed), _p(src), _p(tgt), _p(knn), B, N, C, S, k, int(num_iterations),
+                             _p(sigma), _p(sigma_d), _p(w), _p(it), _p(ws), nb, _stream(normed.device)),
+          "pdsc_nsm_weights")
+    return w, it
+
+
+# ---------------------------------------------------------------------- a9
+def rigid_transform_3d(A, B, weights=None):
+    """[nb,4,4] weighted Kabsch (models/common.py:7-45); A,B [nb,n,3], weights [nb,n]."""
+    A, B = _dev(A, "A"), _dev(B, "B")
+    w = _dev(weights, "weights") if weights is not None else None
+    nb, n, _ = A.shape
+    out = torch.empty((nb, 4, 4), dtype=torch.float32, device=A.device)
+    check(_lib.load().pdsc_rigid_transform_3d(_p(A), _p(B), _p(w), nb, n, _p(out), _stream(A.device)),
+          "pdsc_rigid_transform_3d")
+    return out
+
+
+# --------------------------------------------------------------------- a10
+def seed_hypotheses(src, tgt, knn, weights, tau: float):
+    """(seed_trans [B,S,4,4], fitness [B,S], best [B], trans [B,4,4], labels [B,N])."""
+    src, tgt = _dev(src, "src"), _dev(tgt, "tgt")
+    knn, weights = _dev(knn, "knn", torch.int32), _dev(weights, "weights")
+    B, N, _ = src.shape
+    _, S, k = knn.shape
+    dev = src.device
+    seed_trans = torch.empty((B, S, 4, 4), dtype=torch.float32, device=dev)
+    fitness = torch.empty((B, S), dtype=torch.float32, device=dev)
+    best = torch.empty((B,), dtype=torch.int32, device=dev)
+    trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
+    labels = torch.empty((B, N), dtype=torch.float32, device=dev)
+    check(_lib.load().pdsc_seed_hypotheses(_p(src), _p(tgt), _p(knn), _p(weights), B, N, S, k, float(tau),
+                                           _p(seed_trans), _p(fitness), _p(best), _p(trans), _p(labels),
+                                           _stream(dev)), "pdsc_seed_hypotheses")
+    return seed_trans, fitness, best, trans, labels
+
+
+# --------------------------------------------------------------------- a11
+def post_refine(trans, src, tgt, thr: float):
+    """Refined [B,4,4] (models/PointDSC.py:403-438); `trans` is not modified."""
+    out = _dev(trans, "trans").clone()
+    src, tgt = _dev(src, "src"), _dev(tgt, "tgt")
+    B, N, _ = src.shape
+    check(_lib.load().pdsc_post_refine(_p(out), _p(src), _p(tgt), B, N, float(thr), _stream(src.device)),
+          "pdsc_post_refine")
+    return out
+
+
+# ----------------------------------------------------------------- forward
+def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
+    """Full testing forward for B pairs: (final_trans [B,4,4], final_labels [B,N])
+    (+ (confidence [B,N], seeds [B,S]) when ``debug``)."""
+    corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
+    B, N, _ = src.shape
+    if corr_pos.shape[:2] != (B, N) or tgt.shape != src.shape:
+        raise ValueError(f"shape mismatch corr_pos {tuple(corr_pos.shape)} src {tuple(src.shape)} "
+                         f"tgt {tuple(tgt.shape)}")
+    dev = src.device
+    L = _lib.load()
+    nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
+    if nb == 0:
+        raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
+    ws = _workspace(nb, dev)
+    trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
+    labels = torch.empty((B, N), dtype=torch.float32, device=dev)
+    conf = seeds = None
+    if debug:
+        conf = torch.empty((B, N), dtype=torch.float32, device=dev)
+        seeds = torch.empty((B, int(N * cfg.ratio)), dtype=torch.int32, device=dev)
+    check(L.pdsc_forward_testing(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
+                                 _p(trans), _p(labels), _p(conf), _p(seeds), _p(ws), nb, _stream(dev)),
+          "pdsc_forward_testing")
+    if debug:
+        return trans, labels, conf, seeds
+    return trans, labels
+
+
+class ForwardPlan:
+    """Reusable workspace + outputs for repeated batched forwards of one (B, N).
+
+    Avoids the per-call allocator round trip in throughput loops (bench.py)."""
+
+    def __init__(self, cfg, packed, B, N, device):
+        L = _lib.load()
+        self.cfg, self.packed, self.B, self.N = cfg, packed, B, N
+        self.nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
+        if self.nb == 0:
+            raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
+        self.ws = _workspace(self.nb, device)
+        self.trans = torch.empty((B, 4, 4), dtype=torch.float32, device=device)
+        self.labels = torch.empty((B, N), dtype=torch.float32, device=device)
+
+    def run(self, corr_pos, src, tgt, stream=None):
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream(src.device)
+        check(_lib.load().pdsc_forward_testing(
+            ctypes.byref(self.cfg), _p(self.packed), _p(corr_pos), _p(src), _p(tgt), self.B, self.N,
+            _p(self.trans), _p(self.labels), None, None, _p(self.ws), self.nb, s), "pdsc_forward_testing")
+        return self.trans, self.labels

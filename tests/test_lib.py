@@ -1,0 +1,97 @@
+"""libpdsc.so loads and exports the C ABI of include/pdsc.h; host-side logic
+(argument checks, parameter order, workspace queries) -- no GPU needed."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from pointdsc_amd import _lib
+from pointdsc_amd.synthetic import state_dict_keys
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "pdsc.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(pdsc_[a-z_0-9]+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20, names
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/pdsc.h but not exported"
+    assert set(names) == set(_lib.EXPORTS)
+
+
+def test_version():
+    assert b"gfx950" in _lib.load().pdsc_version()
+
+
+@pytest.mark.parametrize("L", [1, 2, 12])
+def test_param_order_matches_reference_state_dict(L):
+    lib = _lib.load()
+    cfg = _lib.make_config(num_layers=L)
+    names = [lib.pdsc_param_name(ctypes.byref(cfg), i).decode() for i in range(lib.pdsc_param_count(ctypes.byref(cfg)))]
+    ref = [k for k in state_dict_keys(L) if not k.endswith("num_batches_tracked")]
+    assert names == ref
+
+
+def test_refine_threshold_rule():
+    # models/PointDSC.py:415-418
+    assert abs(_lib.make_config(inlier_threshold=0.10).refine_threshold - 0.10) < 1e-7
+    assert abs(_lib.make_config(inlier_threshold=0.6).refine_threshold - 1.2) < 1e-7
+
+
+def test_workspace_queries():
+    lib = _lib.load()
+    cfg = _lib.make_config()
+    for B, N in [(1, 1000), (4, 5000), (1, 30)]:
+        assert lib.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N) > 4 * B * N * N
+        assert lib.pdsc_encoder_workspace_bytes(ctypes.byref(cfg), B, N) > 0
+    assert lib.pdsc_forward_workspace_bytes(ctypes.byref(cfg), 1, 5) == 0  # int(5*0.1) = 0 seeds
+    bad = _lib.make_config(num_channels=64)
+    assert lib.pdsc_forward_workspace_bytes(ctypes.byref(bad), 1, 1000) == 0
+    assert b"num_channels" in lib.pdsc_last_error()
+
+
+def test_argument_errors_without_device():
+    lib = _lib.load()
+    assert lib.pdsc_compat_f32(None, None, 1, 10, None, None, None) == 1
+    assert b"null" in lib.pdsc_last_error()
+    cfg = _lib.make_config()
+    rc = lib.pdsc_forward_testing(ctypes.byref(cfg), None, None, None, None, 1, 1000, None, None, None,
+                                  None, None, 0, None)
+    assert rc == 1
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load()
+
+
+def test_module_state_dict_keys_match_reference():
+    import torch
+    from pointdsc_amd.PointDSC import PointDSC
+    m = PointDSC(num_layers=12)
+    assert list(m.state_dict().keys()) == state_dict_keys(12)
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in
+          __import__("pointdsc_amd.synthetic", fromlist=["x"]).trained_state_dict("3dmatch", 12).items()}
+    m.load_state_dict(sd, strict=True)
+
+
+def test_module_refuses_cpu_and_training():
+    import torch
+    from pointdsc_amd.PointDSC import PointDSC
+    m = PointDSC(num_layers=2)
+    data = {"corr_pos": torch.zeros(1, 50, 6), "src_keypts": torch.zeros(1, 50, 3),
+            "tgt_keypts": torch.zeros(1, 50, 3)}
+    with pytest.raises(NotImplementedError):
+        m(data)
+    data["testing"] = True
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(data)
