@@ -65,6 +65,7 @@ struct Dims {
 
 int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     if (B < 1 || N < 2) return fail(PDSC_ERR_ARG, "B=%d N=%d (need B >= 1, N >= 2)", B, N);
+    if (N > 32767) return fail(PDSC_ERR_UNSUPPORTED, "N=%d > 32767 (32-bit buffer descriptors over M)", N);
     d.B = B;
     d.N = N;
     d.Npad = round_up(N, QB);
@@ -300,7 +301,7 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
                            pdsc_stream_t stream) {
     if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
     if (!q || !k || !v || !M || !msg || !ws) return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    if (B < 1 || N < 1 || N > 32767) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     RET_IF(need_ws(ws_bytes, pdsc_attention_workspace_bytes(B, N, C)));
     hipStream_t s = S_(stream);
     const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
@@ -332,7 +333,7 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nspl
 int32_t pdsc_attention_partials_f32(const float *q, const float *k, const float *v, const float *M,
                                     int32_t B, int32_t N, float *opart, float *ml, pdsc_stream_t stream) {
     if (!q || !k || !v || !M || !opart || !ml) return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    if (B < 1 || N < 1 || N > 32767) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     HIPCHK(launch_attention(q, k, v, M, B, N, round_up(N, QB), attention_nsplit(B, N), opart, ml,
                             S_(stream)));
     return PDSC_OK;

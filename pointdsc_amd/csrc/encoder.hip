@@ -20,7 +20,7 @@
 //   where M is read column-wise (M symmetric => coalesced 128-B rows);
 //   incompatible pairs keep logit 0 (not -inf) exactly as :41; online softmax
 //   with a running max; split-K over keys when B*N is too small to fill 256 CUs.
-#include "pdsc_internal.hpp"
+#include "attention.hpp"
 
 namespace pdsc {
 
@@ -73,184 +73,23 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s) {
 }
 
 // ================================================================= attention
-constexpr int KSTR = CH + 4;  // K tile row stride (floats): conflict-free ds_read_b128 columns
-constexpr int VSTR = CH;
-constexpr size_t ATT_LDS = (size_t)2 * KT * (KSTR + VSTR) * sizeof(float);  // 66,560 B
+// Production variant of attention.hpp: 4 waves x 32 queries per workgroup,
+// 32-key LDS stages, v_exp_f32 on log2e-prescaled logits, XCD-aware block map
+// (A/B-timed against the other variants with tools/attn_bench.hip).
+constexpr int ATT_NW = 4, ATT_KTS = 32;
 
-__global__ __launch_bounds__(256, 2) void attention_kernel(
-    const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
-    const float *__restrict__ M, int N, int Npad, int nsplit, int tps, float *__restrict__ opart,
-    float *__restrict__ ml) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    float *Kl0 = smem, *Kl1 = smem + KT * KSTR;
-    float *Vl0 = smem + 2 * KT * KSTR, *Vl1 = Vl0 + KT * VSTR;
+static AttnGrid prod_grid(int B, int N) { return attention_grid<ATT_NW, ATT_KTS>(B, N, 1024); }
 
-    const int b = blockIdx.z, split = blockIdx.y;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int q0 = blockIdx.x * QB + wave * 32;
-    const int ntiles = (N + KT - 1) / KT;
-    const int t0 = split * tps, t1 = min(ntiles, t0 + tps);
-    const float *Qb = q + (size_t)b * Npad * CH;
-    const float *Kb = k + (size_t)b * Npad * CH;
-    const float *Vb = v + (size_t)b * Npad * CH;
-    const float *Mb = M + (size_t)b * N * N;
-    if (t0 >= t1) {  // empty split (not produced by attention_nsplit): neutral partials
-        const size_t base = (size_t)(b * nsplit + split) * Npad;
-        for (int r = 0; r < 16; ++r)
-            *reinterpret_cast<f32x4 *>(opart + (base + q0 + acc_row(r, h)) * CH + 4 * l32) = f32x4{0, 0, 0, 0};
-        if (h == 0) {
-            ml[(base + q0 + l32) * 2] = -INFINITY;
-            ml[(base + q0 + l32) * 2 + 1] = 0.0f;
-        }
-        return;
-    }
-
-    // This wave's 32 queries as the B operand: lane -> query l32, channels h*64 + i.
-    float qf[64];
-    {
-        const f32x4 *src4 = reinterpret_cast<const f32x4 *>(Qb + (size_t)(q0 + l32) * CH + h * 64);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const f32x4 t = src4[i];
-            qf[4 * i] = t[0];
-            qf[4 * i + 1] = t[1];
-            qf[4 * i + 2] = t[2];
-            qf[4 * i + 3] = t[3];
-        }
-    }
-
-    f32x4 sk[4], sv[4];
-    auto load_tile = [&](int t) {
-        const int key0 = t * KT;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = tid + 256 * i, row = idx >> 5, c4 = idx & 31;
-            sk[i] = *reinterpret_cast<const f32x4 *>(Kb + (size_t)(key0 + row) * CH + 4 * c4);
-            sv[i] = *reinterpret_cast<const f32x4 *>(Vb + (size_t)(key0 + row) * CH + 4 * c4);
-        }
-    };
-    auto store_tile = [&](float *Kl, float *Vl) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int idx = tid + 256 * i, row = idx >> 5, c4 = idx & 31;
-            *reinterpret_cast<f32x4 *>(Kl + row * KSTR + 4 * c4) = sk[i];
-            *reinterpret_cast<f32x4 *>(Vl + row * VSTR + 4 * c4) = sv[i];
-        }
-    };
-
-    f32x16 O0 = zero16(), O1 = zero16(), O2 = zero16(), O3 = zero16();
-    float m_run = -INFINITY, l_run = 0.0f;
-    const float inv_sqrt_c = 0.08838834764831845f;  // 1/sqrt(128) (:39 divides by C**0.5)
-    const int qq = q0 + l32;
-    const bool qvalid = qq < N;
-
-    load_tile(t0);
-    store_tile(Kl0, Vl0);
-    __syncthreads();
-
-    for (int t = t0; t < t1; ++t) {
-        const int buf = (t - t0) & 1;
-        const float *Kl = buf ? Kl1 : Kl0;
-        const float *Vl = buf ? Vl1 : Vl0;
-        const int key0 = t * KT;
-        if (t + 1 < t1) load_tile(t + 1);
-
-        // compatibility weights of this tile: M[q][key] == M[key][q]
-        float mv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + acc_row(r, h);
-            mv[r] = (qvalid && key < N) ? Mb[(size_t)key * N + qq] : 0.0f;
-        }
-
-        // S^T[key][query] = K Q^T
-        f32x16 S = zero16();
-        const float *Kp = Kl + l32 * KSTR + h * 64;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const f32x4 kv = *reinterpret_cast<const f32x4 *>(Kp + 4 * i);
-            S = mfma32(kv[0], qf[4 * i], S);
-            S = mfma32(kv[1], qf[4 * i + 1], S);
-            S = mfma32(kv[2], qf[4 * i + 2], S);
-            S = mfma32(kv[3], qf[4 * i + 3], S);
-        }
-
-        // logits and online softmax (row = query = l32; this lane holds 16 of the 32 keys)
-        float p[16];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int key = key0 + acc_row(r, h);
-            p[r] = (key < N) ? mv[r] * (S[r] * inv_sqrt_c) : -INFINITY;
-            mx = fmaxf(mx, p[r]);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = expf(m_run - m_new);
-        float psum = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            p[r] = expf(p[r] - m_new);
-            psum += p[r];
-        }
-        l_run = l_run * alpha + psum;
-        m_run = m_new;
-        if (!__all(alpha == 1.0f)) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float a = __shfl(alpha, acc_row(r, h));
-                O0[r] *= a;
-                O1[r] *= a;
-                O2[r] *= a;
-                O3[r] *= a;
-            }
-        }
-
-        // O[query][d] += P V, d = 4*l32 + e
-        const float *Vp = Vl + 4 * l32 + 4 * h * VSTR;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const f32x4 vv = *reinterpret_cast<const f32x4 *>(Vp + ((s & 3) + 8 * (s >> 2)) * VSTR);
-            O0 = mfma32(p[s], vv[0], O0);
-            O1 = mfma32(p[s], vv[1], O1);
-            O2 = mfma32(p[s], vv[2], O2);
-            O3 = mfma32(p[s], vv[3], O3);
-        }
-
-        if (t + 1 < t1) store_tile(buf ? Kl0 : Kl1, buf ? Vl0 : Vl1);
-        __syncthreads();
-    }
-
-    l_run += __shfl_xor(l_run, 32);
-    const size_t base = (size_t)(b * nsplit + split) * Npad;
-    float *Ob = opart + base * CH;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = q0 + acc_row(r, h);
-        *reinterpret_cast<f32x4 *>(Ob + (size_t)row * CH + 4 * l32) = f32x4{O0[r], O1[r], O2[r], O3[r]};
-    }
-    if (h == 0) {
-        ml[(base + qq) * 2] = m_run;
-        ml[(base + qq) * 2 + 1] = l_run;
-    }
-}
-
-int attention_nsplit(int B, int N) {
-    const int ntiles = (N + KT - 1) / KT;
-    const int nqb = round_up(N, QB) / QB;
-    const int target = 1024;
-    int ns = (target + B * nqb - 1) / (B * nqb);
-    ns = std::max(1, std::min(ns, std::max(1, ntiles / 4)));
-    const int tps = (ntiles + ns - 1) / ns;
-    return (ntiles + tps - 1) / tps;
-}
+int attention_nsplit(int B, int N) { return prod_grid(B, N).nsplit; }
 
 hipError_t launch_attention(const float *q, const float *k, const float *v, const float *M, int B,
                             int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s) {
-    const int ntiles = (N + KT - 1) / KT;
-    const int tps = (ntiles + nsplit - 1) / nsplit;
-    hipLaunchKernelGGL(attention_kernel, dim3(Npad / QB, nsplit, B), dim3(256), ATT_LDS, s, q, k, v,
-                       M, N, Npad, nsplit, tps, opart, ml);
+    const AttnGrid g = prod_grid(B, N);
+    if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
+    const size_t lds = attention_lds_bytes<ATT_NW, ATT_KTS>();
+    auto kern = attention_kernel_t<ATT_NW, ATT_KTS, true, true>;
+    hipLaunchKernelGGL(kern, dim3(g.B * g.nqb * g.nsplit), dim3(ATT_NW * 64), lds, s, q, k, v, M, g,
+                       opart, ml);
     return hipGetLastError();
 }
 
