@@ -103,6 +103,13 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
  * pdsc_attention_layout); outputs the split partials opart [B,nsplit,Npad,C]
  * (unnormalised) and ml [B,nsplit,Npad,2] (running max, sum).               */
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit);
+
+/* Measurement hook (bench.py): while capacity > 0, every attention launch the
+ * encoder issues from the calling thread records start_events[i] / stop_events[i]
+ * (hipEvent_t) around itself on its stream, i = (*count)++ while < capacity.
+ * Pass capacity 0 to disable.  The caller owns the events and the counter.   */
+int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_events, int32_t capacity,
+                              int32_t *count);
 int32_t pdsc_attention_partials_f32(const float *q_pad, const float *k_pad, const float *v_pad,
                                     const float *M, int32_t B, int32_t N, float *opart, float *ml,
                                     pdsc_stream_t stream);
@@ -154,10 +161,12 @@ int32_t pdsc_rigid_transform_3d(const float *A, const float *Bp, const float *w,
  * the best hypothesis.  Replaces models/PointDSC.py:287-335.
  * seed_trans [B,S,4,4] and fitness [B,S] are required (they host the per-seed
  * scratch); best [B] int32 (may be NULL); trans [B,4,4]; labels [B,N].      */
+size_t pdsc_seed_hypotheses_workspace_bytes(int32_t B, int32_t S);
 int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *knn,
                              const float *weights, int32_t B, int32_t N, int32_t S, int32_t k,
                              float tau, float *seed_trans, float *fitness, int32_t *best,
-                             float *trans, float *labels, pdsc_stream_t stream);
+                             float *trans, float *labels, void *workspace, size_t workspace_bytes,
+                             pdsc_stream_t stream);
 
 /* ------------------------------------------------ a11 post-refinement ------
  * <= 20 IRLS re-fits on the inliers of |R src + t - tgt| < thr with weights

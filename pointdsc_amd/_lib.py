@@ -48,6 +48,7 @@ _PROTOS = {
     "pdsc_attention_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "pdsc_attention_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
     "pdsc_attention_layout": (c_int32, [c_int32, c_int32, ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)]),
+    "pdsc_attention_timing": (c_int32, [ctypes.POINTER(vp), ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_attention_partials_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp]),
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
     "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
@@ -56,8 +57,9 @@ _PROTOS = {
     "pdsc_nsm_weights": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                    vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_rigid_transform_3d": (c_int32, [vp, vp, vp, c_int32, c_int32, vp, vp]),
+    "pdsc_seed_hypotheses_workspace_bytes": (c_size_t, [c_int32, c_int32]),
     "pdsc_seed_hypotheses": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_float,
-                                       vp, vp, vp, vp, vp, vp]),
+                                       vp, vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_post_refine": (c_int32, [vp, vp, vp, c_int32, c_int32, c_float, vp]),
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,

@@ -16,6 +16,11 @@ namespace {
 thread_local std::string g_err;
 thread_local std::string g_name;
 
+// measurement hook (pdsc_attention_timing): events recorded around attention launches
+thread_local hipEvent_t *g_tstart = nullptr, *g_tstop = nullptr;
+thread_local int g_tcap = 0;
+thread_local int32_t *g_tcount = nullptr;
+
 int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -52,7 +57,7 @@ int check_cfg(const pdsc_config *cfg) {
         return fail(PDSC_ERR_UNSUPPORTED, "num_channels=%d: only %d is implemented", cfg->num_channels, CH);
     if (cfg->num_layers < 1 || cfg->num_layers > 64)
         return fail(PDSC_ERR_UNSUPPORTED, "num_layers=%d not in [1, 64]", cfg->num_layers);
-    if (cfg->in_dim < 1 || cfg->in_dim > 64) return fail(PDSC_ERR_UNSUPPORTED, "in_dim=%d", cfg->in_dim);
+    if (cfg->in_dim < 1 || cfg->in_dim > 16) return fail(PDSC_ERR_UNSUPPORTED, "in_dim=%d not in [1, 16]", cfg->in_dim);
     if (cfg->num_iterations < 0 || cfg->num_iterations > 31)
         return fail(PDSC_ERR_UNSUPPORTED, "num_iterations=%d not in [0, 31]", cfg->num_iterations);
     if (cfg->k < 1) return fail(PDSC_ERR_ARG, "k=%d", cfg->k);
@@ -74,7 +79,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     d.T = cfg->num_iterations;
     d.nsplit = attention_nsplit(B, N);
     if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
-    if (d.k > 64) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 64", d.k);
+    if (d.k > 63) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 63", d.k);
     return PDSC_OK;
 }
 
@@ -99,7 +104,10 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                 hipStream_t s) {
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
     for (int l = 0; l < lay.L; ++l) {
+        const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
+        if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
         HIPCHK(launch_attention(e.q, e.k, e.v, M, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         if (l + 1 < lay.L)
             HIPCHK(launch_pw_mid(packed, lay, l, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
                                  e.k, e.v, s));
@@ -111,12 +119,13 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
 }
 
 struct NsmBufs {
-    float *hist, *weights;
+    float *hist, *weights, *T;
     unsigned *mask;
 };
 
 NsmBufs carve_nsm(Carve &c, int B, int S, int k, int T) {
     NsmBufs n;
+    n.T = c.take<float>((size_t)B * S * k * k);
     n.hist = c.take<float>((size_t)B * S * std::max(T, 1) * k);
     n.mask = c.take<unsigned>((size_t)B);
     n.weights = c.take<float>((size_t)B * S * k);
@@ -128,13 +137,13 @@ int run_nsm(const float *normed, const float *src, const float *tgt, const int *
             float *weights, int *iters, hipStream_t s) {
     HIPCHK(hipMemsetAsync(nb.mask, 0xff, sizeof(unsigned) * B, s));
     if (T > 0)
-        HIPCHK(launch_nsm_power(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
+        HIPCHK(launch_nsm_power(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.T, nb.hist, nb.mask, s));
     HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, weights, iters, s));
     return PDSC_OK;
 }
 
 struct FwdBufs {
-    float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights;
+    float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights, *hsums;
     int *seeds, *knn, *counts;
     EncBufs enc;
     NsmBufs nsm;
@@ -154,6 +163,7 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.weights = f.nsm.weights;
     f.seed_trans = c.take<float>((size_t)d.B * d.S * 16);
     f.counts = c.take<int>((size_t)d.B * d.S);
+    f.hsums = c.take<float>((size_t)d.B * d.S * 15);
     return f;
 }
 
@@ -323,6 +333,17 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     return PDSC_OK;
 }
 
+int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_events, int32_t capacity,
+                              int32_t *count) {
+    if (capacity > 0 && (!start_events || !stop_events || !count))
+        return fail(PDSC_ERR_ARG, "null events/count with capacity %d", capacity);
+    g_tstart = reinterpret_cast<hipEvent_t *>(const_cast<void **>(start_events));
+    g_tstop = reinterpret_cast<hipEvent_t *>(const_cast<void **>(stop_events));
+    g_tcap = capacity;
+    g_tcount = count;
+    return PDSC_OK;
+}
+
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit) {
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
@@ -360,7 +381,7 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
                       pdsc_stream_t stream) {
     if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
     if (!normed || !seeds || !knn || !ws) return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || S < 1 || k < 1 || k + 1 > N || k > 255) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
+    if (B < 1 || S < 1 || k < 1 || k + 1 > N || k > 63) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
     RET_IF(need_ws(ws_bytes, pdsc_seed_knn_workspace_bytes(B, N, S)));
     hipStream_t s = S_(stream);
     float *dist = static_cast<float *>(ws);
@@ -400,10 +421,14 @@ int32_t pdsc_rigid_transform_3d(const float *A, const float *Bp, const float *w,
 }
 
 // ------------------------------------------------------------------- a10
+size_t pdsc_seed_hypotheses_workspace_bytes(int32_t B, int32_t S) {
+    return align_bytes((size_t)B * S * 15 * sizeof(float));
+}
+
 int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *knn, const float *weights,
                              int32_t B, int32_t N, int32_t S, int32_t k, float tau, float *seed_trans,
-                             float *fitness, int32_t *best, float *trans, float *labels,
-                             pdsc_stream_t stream) {
+                             float *fitness, int32_t *best, float *trans, float *labels, void *ws,
+                             size_t ws_bytes, pdsc_stream_t stream) {
     if (!src || !tgt || !knn || !weights || !trans || !labels || !seed_trans)
         return fail(PDSC_ERR_ARG, "null pointer (seed_trans is required as scratch)");
     if (B < 1 || N < 1 || S < 1 || k < 1 || k > 64) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
@@ -412,7 +437,10 @@ int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *
     // each into count / N (same thread, same element)
     if (!fitness) return fail(PDSC_ERR_ARG, "fitness [B,S] buffer is required (hosts the inlier counts)");
     int *counts = reinterpret_cast<int *>(fitness);
-    HIPCHK(launch_hypotheses(src, tgt, knn, weights, B, N, S, k, tau, seed_trans, counts, s));
+    if (!ws || ws_bytes < pdsc_seed_hypotheses_workspace_bytes(B, S))
+        return fail(PDSC_ERR_ARG, "workspace too small");
+    HIPCHK(launch_hypotheses(src, tgt, knn, weights, B, N, S, k, tau, seed_trans, counts,
+                             static_cast<float *>(ws), s));
     HIPCHK(launch_select_best(src, tgt, seed_trans, counts, B, N, S, tau, fitness, best, trans, labels, s));
     return PDSC_OK;
 }
@@ -466,7 +494,7 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
                    nullptr, s));
     // a9-a10 (:287-335)
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
-                             f.seed_trans, f.counts, s));
+                             f.seed_trans, f.counts, f.hsums, s));
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
                               nullptr, nullptr, final_trans, final_labels, s));
     // a11 (:186, :403-438)

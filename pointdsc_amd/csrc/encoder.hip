@@ -136,55 +136,79 @@ hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N
 }
 
 // ============================================================ pointwise chain
-// Dense layer on a PT=32-point tile held in LDS: Y = epi(X W^T + b).  Waves take
-// 32-column output tiles round-robin.  A operand = X rows (lane -> point),
-// B operand = packed W (one 1-KiB coalesced load per 4 MFMAs).
+// A workgroup (4 waves) owns PT = 64 points (two 32-row MFMA tiles) held in LDS
+// and runs the whole per-point chain between two attention launches.
+// Dense layer Y = epi(X W^T + b): A operand = X rows (lane -> point), B operand
+// = packed W (one coalesced 1-KiB load per 4 MFMAs).  Wide layers (>= 128
+// outputs): each wave owns column tiles and computes BOTH row tiles, so every
+// weight fragment feeds two MFMAs; narrow layers (32/64 outputs): one
+// (row tile, column tile) per wave so all four waves stay busy.
 enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
 
-template <int IN, int OUT, int EPI>
-PDSC_DEV void dense32(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off,
-                      float *Y, int ystr, const float *__restrict__ resid, int wave, int lane) {
+constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
+constexpr int IN_MAX = 16;  // layer0 input width held in registers
+
+template <int IN, int EPI, int NRT>
+PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off,
+                         int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
-    for (int jt = wave; jt < OUT / 32; jt += 4) {
-        f32x16 acc = zero16();
-        const float *xp = X + l32 * xstr + h * (IN / 2);
-        const f32x4 *wp = reinterpret_cast<const f32x4 *>(pk + off.w) + (size_t)jt * (IN / 8) * 64 + lane;
-#pragma unroll 4
-        for (int g = 0; g < IN / 8; ++g) {
-            const f32x4 xa = *reinterpret_cast<const f32x4 *>(xp + 4 * g);
-            const f32x4 wb = wp[g * 64];
-            acc = mfma32(xa[0], wb[0], acc);
-            acc = mfma32(xa[1], wb[1], acc);
-            acc = mfma32(xa[2], wb[2], acc);
-            acc = mfma32(xa[3], wb[3], acc);
+    f32x16 acc[NRT];
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) acc[i] = zero16();
+    const float *xp = X + (rt0 * 32 + l32) * xstr + h * (IN / 2);
+    const f32x4 *wp = reinterpret_cast<const f32x4 *>(pk + off.w) + (size_t)ct * (IN / 8) * 64 + lane;
+    f32x4 wbuf[IN / 8];  // the wave's whole weight panel, issued up front
+#pragma unroll
+    for (int g = 0; g < IN / 8; ++g) wbuf[g] = wp[g * 64];
+#pragma unroll
+    for (int g = 0; g < IN / 8; ++g) {
+        const f32x4 wb = wbuf[g];
+#pragma unroll
+        for (int i = 0; i < NRT; ++i) {
+            const f32x4 xa = *reinterpret_cast<const f32x4 *>(xp + i * 32 * xstr + 4 * g);
+            acc[i] = mfma32(xa[0], wb[0], acc[i]);
+            acc[i] = mfma32(xa[1], wb[1], acc[i]);
+            acc[i] = mfma32(xa[2], wb[2], acc[i]);
+            acc[i] = mfma32(xa[3], wb[3], acc[i]);
         }
-        const int j = jt * 32 + l32;
-        const float bias = pk[off.bias + j];
-        const float al = pk[off.alpha + j], be = pk[off.beta + j];
+    }
+    const int j = ct * 32 + l32;
+    const float bias = pk[off.bias + j];
+    const float al = pk[off.alpha + j], be = pk[off.beta + j];
+#pragma unroll
+    for (int i = 0; i < NRT; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = acc_row(r, h);
-            float y = acc[r] + bias;
-            if (EPI == EPI_BN_RELU) y = fmaxf(y * al + be, 0.0f);
+            const int row = (rt0 + i) * 32 + acc_row(r, h);
+            float y = acc[i][r] + bias;
+            if (EPI == EPI_BN_RELU) y = fmaxf(y * al + be, 0.0f);  // eval BN as torch folds it, ReLU
             if (EPI == EPI_RELU) y = fmaxf(y, 0.0f);
-            if (EPI == EPI_RESID) y = resid[row * CH + j] + y;  // res = feat + message (:44)
+            if (EPI == EPI_RESID) y = resid[row * CH + j] + y;      // res = feat + message (:44)
             Y[row * ystr + j] = y;
         }
+}
+
+template <int IN, int OUT, int EPI>
+PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, float *Y,
+                      int ystr, const float *__restrict__ resid, int wave, int lane) {
+    constexpr int NCT = OUT / 32;
+    if constexpr (NCT >= 4) {
+        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, EPI, 2>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
+    } else {
+        const int rt = wave & 1, ct = wave >> 1;
+        if (ct < NCT) dense_tile<IN, EPI, 1>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
     }
 }
 
-// Copy a [32][CH] LDS tile (stride xstr) to global rows [p0, p0+32) of dst (row stride CH).
-PDSC_DEV void store_tile32(const float *X, int xstr, float *__restrict__ dst, int p0, int nrows, int tid) {
-    for (int e = tid; e < 32 * (CH / 4); e += 256) {
+// Copy a [PT][CH] LDS tile (stride xstr) to global rows [p0, p0 + nrows) (row stride CH).
+PDSC_DEV void store_rows(const float *X, int xstr, float *__restrict__ dst, int p0, int nrows, int tid) {
+    for (int e = tid; e < PT * (CH / 4); e += 256) {
         const int p = e / (CH / 4), c4 = e % (CH / 4);
         if (p < nrows)
             *reinterpret_cast<f32x4 *>(dst + (size_t)(p0 + p) * CH + 4 * c4) =
                 *reinterpret_cast<const f32x4 *>(X + p * xstr + 4 * c4);
     }
 }
-
-constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
-constexpr int PW_LDS_FLOATS = 2 * PT * S132 + 2 * PT * S68 + 2 * PT * S36 + 64;
 
 struct PwDense4 {  // PointCN + Q/K/V of one layer
     DenseOff pcn, q, k, v;
@@ -193,19 +217,24 @@ struct PwMsg {  // fc_message of one layer
     DenseOff fc0, fc3, fc6;
 };
 
-// PointCN_l then Q/K/V_l of the tile in Xin -> feat (global), Q, K, V (global).
+// LDS: A, B = [PT][S132] (67,584 B -> 2 workgroups per CU).  The fc_message
+// hidden tile C [PT][S68] and pw_first's corr_pos tile live in B, which is free
+// until the residual add writes it.
+constexpr size_t PW_LDS = (size_t)(2 * PT * S132) * sizeof(float);
+
+// PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> global); Xout rows -> feat.
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, float *__restrict__ Q, float *__restrict__ K,
                       float *__restrict__ V, int p0, int tid, int wave, int lane) {
-    dense32<CH, CH, EPI_BN_RELU>(Xin, S132, pk, d.pcn, Xout, S132, nullptr, wave, lane);
+    dense64<CH, CH, EPI_BN_RELU>(Xin, S132, pk, d.pcn, Xout, S132, nullptr, wave, lane);
     __syncthreads();
-    store_tile32(Xout, S132, feat, p0, 32, tid);
-    dense32<CH, CH, EPI_BIAS>(Xout, S132, pk, d.q, Q + (size_t)p0 * CH, CH, nullptr, wave, lane);
-    dense32<CH, CH, EPI_BIAS>(Xout, S132, pk, d.k, K + (size_t)p0 * CH, CH, nullptr, wave, lane);
-    dense32<CH, CH, EPI_BIAS>(Xout, S132, pk, d.v, V + (size_t)p0 * CH, CH, nullptr, wave, lane);
+    store_rows(Xout, S132, feat, p0, PT, tid);
+    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.q, Q + (size_t)p0 * CH, CH, nullptr, wave, lane);
+    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.k, K + (size_t)p0 * CH, CH, nullptr, wave, lane);
+    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.v, V + (size_t)p0 * CH, CH, nullptr, wave, lane);
 }
 
-// layer0 (Conv1d in_dim -> 128) + PointCN_0 + QKV_0.
+// layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
 __global__ __launch_bounds__(256) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
                                                        size_t l0b, PwDense4 d,
                                                        const float *__restrict__ corr, int in_dim,
@@ -213,7 +242,7 @@ __global__ __launch_bounds__(256) void pw_first_kernel(const float *__restrict__
                                                        float *__restrict__ Q, float *__restrict__ K,
                                                        float *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *X0 = sm, *X1 = sm + PT * S132, *cp = sm + 2 * PT * S132;  // cp: [PT][in_dim]
+    float *XA = sm, *XB = sm + PT * S132, *cp = XB;  // cp: [PT][in_dim], consumed before XB is written
     const int b = blockIdx.y, p0 = blockIdx.x * PT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
@@ -221,37 +250,49 @@ __global__ __launch_bounds__(256) void pw_first_kernel(const float *__restrict__
         const int p = e / in_dim;
         cp[e] = (p0 + p < N) ? corr[((size_t)b * N + p0) * in_dim + e] : 0.0f;
     }
+    // thread -> output channel j (both halves of the block cover rows of opposite parity)
+    const int j = tid & (CH - 1), p_off = tid >> 7;
+    float w[IN_MAX];
+#pragma unroll
+    for (int c = 0; c < IN_MAX; ++c) w[c] = (c < in_dim) ? pk[l0w + j * in_dim + c] : 0.0f;
+    const float bj = pk[l0b + j];
     __syncthreads();
-    for (int e = tid; e < PT * CH; e += 256) {
-        const int p = e / CH, j = e % CH;
+    for (int p = p_off; p < PT; p += 2) {
         float s = 0.0f;
-        for (int c = 0; c < in_dim; ++c) s = __builtin_fmaf(pk[l0w + j * in_dim + c], cp[p * in_dim + c], s);
-        X0[p * S132 + j] = s + pk[l0b + j];
+#pragma unroll
+        for (int c = 0; c < IN_MAX; ++c)
+            if (c < in_dim) s = __builtin_fmaf(w[c], cp[p * in_dim + c], s);
+        XA[p * S132 + j] = s + bj;
     }
     __syncthreads();
-    pcn_qkv(X0, X1, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
+    pcn_qkv(XA, XB, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
 }
 
-// combine partials (rows p0..p0+31) into X (stride S132)
+// Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
 PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restrict__ ml, int b,
                            int nsplit, int Npad, int p0, float *X, int tid) {
-    const int p = tid >> 3, d0 = (tid & 7) * 16;
-    float out[16];
-    combine16(opart, ml, b, nsplit, Npad, p0 + p, d0, out);
+    const int p = tid >> 2;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<f32x4 *>(X + p * S132 + d0 + 4 * i) =
-            f32x4{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    for (int half = 0; half < 2; ++half) {
+        const int d0 = (tid & 3) * 32 + half * 16;
+        float out[16];
+        combine16(opart, ml, b, nsplit, Npad, p0 + p, d0, out);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<f32x4 *>(X + p * S132 + d0 + 4 * i) =
+                f32x4{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    }
 }
 
-// message MLP + residual: X (msg) -> R (= feat + fc_message(msg)), scratch H1/H2.
-PDSC_DEV void message_resid(const float *X, float *H1, float *H2, float *R, const float *__restrict__ pk,
-                            const PwMsg &m, const float *__restrict__ feat_rows, int wave, int lane) {
-    dense32<CH, CH2, EPI_BN_RELU>(X, S132, pk, m.fc0, H1, S68, nullptr, wave, lane);
+// fc_message + residual (:43-44): X = msg (A) -> C -> A (stride S68) -> R (B);
+// C may alias R: it is dead once fc3 has read it (barrier before fc6).
+PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restrict__ pk, const PwMsg &m,
+                            const float *__restrict__ feat_rows, int wave, int lane) {
+    dense64<CH, CH2, EPI_BN_RELU>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
     __syncthreads();
-    dense32<CH2, CH2, EPI_BN_RELU>(H1, S68, pk, m.fc3, H2, S68, nullptr, wave, lane);
+    dense64<CH2, CH2, EPI_BN_RELU>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
     __syncthreads();
-    dense32<CH2, CH, EPI_RESID>(H2, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
+    dense64<CH2, CH, EPI_RESID>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
     __syncthreads();
 }
 
@@ -262,13 +303,13 @@ __global__ __launch_bounds__(256) void pw_mid_kernel(const float *__restrict__ p
                                                      float *__restrict__ Q, float *__restrict__ K,
                                                      float *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *XA = sm, *XB = sm + PT * S132, *H1 = sm + 2 * PT * S132, *H2 = H1 + PT * S68;
+    float *XA = sm, *XB = sm + PT * S132, *XC = XB;
     const int b = blockIdx.y, p0 = blockIdx.x * PT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
     combine_tile(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid(XA, H1, H2, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    message_resid(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     pcn_qkv(XB, XA, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
 }
 
@@ -278,42 +319,41 @@ __global__ __launch_bounds__(256) void pw_last_kernel(
     const float *__restrict__ feat, float *__restrict__ feat_out, float *__restrict__ normed,
     float *__restrict__ conf) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *XA = sm, *XB = sm + PT * S132, *H1 = sm + 2 * PT * S132, *H2 = H1 + PT * S68;
-    float *C1 = H2 + PT * S68, *C2 = C1 + PT * S36;
+    float *XA = sm, *XB = sm + PT * S132, *XC = XB;
+    float *C1 = XA, *C2 = XA + PT * S36;  // classifier hidden layers reuse A
     const int b = blockIdx.y, p0 = blockIdx.x * PT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
     const int nrows = min(PT, N - p0);
     combine_tile(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid(XA, H1, H2, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    message_resid(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     // XB = corr_features rows
-    if (feat_out) store_tile32(XB, S132, feat_out + (size_t)b * N * CH, p0, nrows, tid);
-    {   // F.normalize(p=2, dim=-1, eps=1e-12) (:156); 8 lanes per point
-        const int p = tid >> 3, d0 = (tid & 7) * 16;
+    if (feat_out) store_rows(XB, S132, feat_out + (size_t)b * N * CH, p0, nrows, tid);
+    {   // F.normalize(p=2, dim=-1, eps=1e-12) (:156); 4 lanes per point
+        const int p = tid >> 2, d0 = (tid & 3) * 32;
         float ss = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < 32; ++i) {
             const float x = XB[p * S132 + d0 + i];
             ss = __builtin_fmaf(x, x, ss);
         }
         ss += __shfl_xor(ss, 1);
         ss += __shfl_xor(ss, 2);
-        ss += __shfl_xor(ss, 4);
         const float den = fmaxf(sqrtf(ss), 1e-12f);
         if (p < nrows) {
             float *dst = normed + ((size_t)b * N + p0 + p) * CH + d0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 8; ++i)
                 *reinterpret_cast<f32x4 *>(dst + 4 * i) =
                     f32x4{XB[p * S132 + d0 + 4 * i] / den, XB[p * S132 + d0 + 4 * i + 1] / den,
                           XB[p * S132 + d0 + 4 * i + 2] / den, XB[p * S132 + d0 + 4 * i + 3] / den};
         }
     }
     // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171)
-    dense32<CH, CLS, EPI_RELU>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
+    dense64<CH, CLS, EPI_RELU>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
     __syncthreads();
-    dense32<CLS, CLS, EPI_RELU>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
+    dense64<CLS, CLS, EPI_RELU>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
     __syncthreads();
     if (tid < nrows) {
         float s = 0.0f;
@@ -327,8 +367,8 @@ static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
                            int N, int Npad, float *feat, float *q, float *k, float *v, hipStream_t s) {
-    const size_t lds = (size_t)(2 * PT * S132 + PT * lay.in_dim) * sizeof(float);
-    hipLaunchKernelGGL(pw_first_kernel, dim3(Npad / PT, B), dim3(256), lds, s, packed, lay.l0_w,
+    if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pw_first_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed, lay.l0_w,
                        lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
     return hipGetLastError();
 }
@@ -336,8 +376,7 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, float *q,
                          float *k, float *v, hipStream_t s) {
-    const size_t lds = (size_t)(2 * PT * S132 + 2 * PT * S68) * sizeof(float);
-    hipLaunchKernelGGL(pw_mid_kernel, dim3(Npad / PT, B), dim3(256), lds, s, packed,
+    hipLaunchKernelGGL(pw_mid_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed,
                        msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N,
                        Npad, feat, q, k, v);
     return hipGetLastError();
@@ -346,8 +385,7 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, float *conf, hipStream_t s) {
-    const size_t lds = (size_t)(2 * PT * S132 + 2 * PT * S68 + 2 * PT * S36) * sizeof(float);
-    hipLaunchKernelGGL(pw_last_kernel, dim3((N + PT - 1) / PT, B), dim3(256), lds, s, packed,
+    hipLaunchKernelGGL(pw_last_kernel, dim3((N + PT - 1) / PT, B), dim3(256), PW_LDS, s, packed,
                        msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml,
                        nsplit, N, Npad, feat, feat_out, normed, conf);
     return hipGetLastError();

@@ -2,10 +2,10 @@
 // post-refinement.
 //
 //   knn_dist     a6  seed rows of 2 - 2 F F^T (v_mfma_f32_32x32x2_f32), [B][S][N]
-//   knn_select   a6  topk(k+1, smallest)[1:] per seed row: 4-pass 8-bit radix
-//                    select + ordered tie resolution (ascending index)
-//   nsm_power    a7-a8  gather k neighbours, k x k feature*spatial consistency,
-//                    all num_iterations power iterates + per-iterate allclose flags
+//   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed):
+//                    4-pass 8-bit radix select + ordered ballot compaction
+//   nsm_local    a7  gather k neighbours, k x k feature*spatial consistency T
+//   nsm_iter     a8  all num_iterations power iterates + per-iterate allclose flags
 //   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
 //                    is allclose (torch.allclose over the whole batch, :354)
 //   hypotheses   a9-a10  weighted Kabsch per seed (fp64 3x3 SVD on device) +
@@ -74,117 +74,107 @@ PDSC_DEV uint32_t fkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-constexpr int SEL_MAX = 256;  // k + 1 <= SEL_MAX
-
-// topk(k+1, smallest) of one seed row, sorted (key asc, index asc), first dropped.
+// topk(k+1, smallest) of one seed row, one WAVE per seed (4 per workgroup):
+// four 8-bit radix passes find the (k+1)-th smallest key T exactly (per-wave
+// LDS histogram, shuffle scan); one ordered pass then collects every key < T
+// and the first `need` keys == T in index order (ballot + popcount
+// compaction); the k+1 candidates are ranked by (key, index) and the first is
+// dropped positionally (models/common.py:68).  k + 1 <= 64.
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int N, int S,
                                                          int k, int *__restrict__ knn) {
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t sel_bin, sel_need;
-    __shared__ uint32_t cnt_less[256], cnt_eq[256];
-    __shared__ uint32_t lkey[SEL_MAX];
-    __shared__ int lidx[SEL_MAX];
-    const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
+    __shared__ uint32_t hist[4][256];
+    __shared__ uint32_t ckey[4][64];
+    __shared__ int cidx[4][64];
+    const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int s = blockIdx.x * 4 + wave;
+    if (s >= S) return;  // wave-uniform; no workgroup barriers below
     const float *row = dist + ((size_t)b * S + s) * N;
-    const int want = k + 1;
+    uint32_t *h = hist[wave];
+    const uint32_t want = k + 1;
     uint32_t need = want, prefix = 0, mask = 0;
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 24 - 8 * pass;
-        hist[tid] = 0;
-        __syncthreads();
-        for (int j = tid; j < N; j += 256) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) h[lane + 64 * e] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (int j = lane; j < N; j += 64) {
             const uint32_t u = fkey(row[j]);
-            if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+            if ((u & mask) == prefix) atomicAdd(&h[(u >> shift) & 255u], 1u);
         }
-        __syncthreads();
-        if (tid < 64) {
-            uint32_t c[4], tot = 0;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t c[4], tot = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            c[e] = h[4 * lane + e];
+            tot += c[e];
+        }
+        uint32_t incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t base = incl - tot;
+        uint32_t my_bin = 0, my_need = 0;
+        const bool hit = base < need && need <= incl;
+        if (hit) {
+            uint32_t cum = base;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                c[e] = hist[4 * tid + e];
-                tot += c[e];
-            }
-            uint32_t incl = tot;  // inclusive scan over lanes
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if (tid >= o) incl += y;
-            }
-            uint32_t base = incl - tot;
-            if (base < need && need <= incl) {
-                uint32_t cum = base;
-                for (int e = 0; e < 4; ++e) {
-                    if (cum + c[e] >= need) {
-                        sel_bin = 4 * tid + e;
-                        sel_need = need - cum;
-                        break;
-                    }
-                    cum += c[e];
+                if (my_need == 0 && cum + c[e] >= need) {
+                    my_bin = 4 * lane + e;
+                    my_need = need - cum;
                 }
+                cum += c[e];
             }
         }
-        __syncthreads();
-        prefix |= sel_bin << shift;
+        const int src_lane = __ffsll((unsigned long long)__ballot(hit)) - 1;
+        const uint32_t bin = __shfl(my_bin, src_lane);
+        need = __shfl(my_need, src_lane);
+        prefix |= bin << shift;
         mask |= 255u << shift;
-        need = sel_need;
-        __syncthreads();
     }
-    // prefix = threshold key T; take all keys < T and the `need` lowest-index keys == T.
-    const int chunk = (N + 255) / 256;
-    const int jb = tid * chunk, je = min(N, jb + chunk);
-    uint32_t nl = 0, ne = 0;
-    for (int j = jb; j < je; ++j) {
-        const uint32_t u = fkey(row[j]);
-        nl += u < prefix;
-        ne += u == prefix;
-    }
-    cnt_less[tid] = nl;
-    cnt_eq[tid] = ne;
-    __syncthreads();
-    if (tid == 0) {  // exclusive scans (256 entries)
-        uint32_t a = 0, e = 0;
-        for (int t = 0; t < 256; ++t) {
-            const uint32_t x = cnt_less[t], y = cnt_eq[t];
-            cnt_less[t] = a;
-            cnt_eq[t] = e;
-            a += x;
-            e += y;
-        }
-    }
-    __syncthreads();
-    uint32_t pl = cnt_less[tid], pe = cnt_eq[tid];
+    // prefix = T: take all keys < T and the `need` lowest-index keys == T, in index order
     const uint32_t nless = want - need;
-    for (int j = jb; j < je; ++j) {
-        const uint32_t u = fkey(row[j]);
-        if (u < prefix) {
-            if (pl < (uint32_t)want) {
-                lkey[pl] = u;
-                lidx[pl] = j;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t pl = 0, pe = 0;
+    for (int j0 = 0; j0 < N && (pl < nless || pe < need); j0 += 64) {
+        const int j = j0 + lane;
+        const uint32_t u = (j < N) ? fkey(row[j]) : 0xffffffffu;
+        const bool less = j < N && u < prefix, eq = j < N && u == prefix;
+        const unsigned long long lm = __ballot(less), em = __ballot(eq);
+        if (less) {
+            const uint32_t pos = pl + __popcll(lm & below);
+            if (pos < want) {
+                ckey[wave][pos] = u;
+                cidx[wave][pos] = j;
             }
-            ++pl;
-        } else if (u == prefix) {
-            if (pe < need) {
-                lkey[nless + pe] = u;
-                lidx[nless + pe] = j;
-            }
-            ++pe;
         }
+        if (eq) {
+            const uint32_t r = pe + __popcll(em & below);
+            if (r < need) {
+                ckey[wave][nless + r] = u;
+                cidx[wave][nless + r] = j;
+            }
+        }
+        pl += __popcll(lm);
+        pe += __popcll(em);
     }
-    __syncthreads();
-    if (tid < want) {
-        const uint32_t ku = lkey[tid];
-        const int ki = lidx[tid];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < (int)want) {
+        const uint32_t ku = ckey[wave][lane];
+        const int ki = cidx[wave][lane];
         int rank = 0;
-        for (int m = 0; m < want; ++m) {
-            const uint32_t mu = lkey[m];
-            rank += (mu < ku) || (mu == ku && lidx[m] < ki);
+        for (int m = 0; m < (int)want; ++m) {
+            const uint32_t mu = ckey[wave][m];
+            rank += (mu < ku) || (mu == ku && cidx[wave][m] < ki);
         }
         if (rank > 0) knn[((size_t)b * S + s) * k + rank - 1] = ki;  // drop position 0 (:68)
     }
 }
 
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s) {
-    hipLaunchKernelGGL(knn_select_kernel, dim3(S, B), dim3(256), 0, s, dist, N, S, k, knn);
+    hipLaunchKernelGGL(knn_select_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, dist, N, S, k, knn);
     return hipGetLastError();
 }
 
@@ -192,31 +182,30 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
 constexpr int KMAX = 64;
 constexpr int FSTR = CH + 4;
 
-// One workgroup per (seed, pair).  hist[b][s][t][a] = iterate t+1, lane a.
-// Bit t of the seed's flag word = allclose(v_{t+1}, v_t); AND-ed into pair_mask[b].
-__global__ __launch_bounds__(256) void nsm_power_kernel(const float *__restrict__ normed,
+// nsm_local: one workgroup per (seed, pair) builds the k x k matrix T of the
+// seed's neighbourhood into Tg[b][s][k][k].
+__global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict__ normed,
                                                         const float *__restrict__ src,
                                                         const float *__restrict__ tgt,
                                                         const int *__restrict__ knn, int N, int S,
-                                                        int k, int T, const float *__restrict__ sigma_p,
+                                                        int k, const float *__restrict__ sigma_p,
                                                         const float *__restrict__ sigma_d_p,
-                                                        float *__restrict__ hist,
-                                                        unsigned *__restrict__ pair_mask) {
+                                                        float *__restrict__ Tg) {
     __shared__ __attribute__((aligned(16))) float F[KMAX * FSTR];
     __shared__ float P[KMAX][6];
-    __shared__ float Tm[KMAX][KMAX + 1];
-    __shared__ float vbuf[KMAX];
     __shared__ int nidx[KMAX];
+    float *Tb = Tg + ((size_t)blockIdx.y * S + blockIdx.x) * k * k;
     const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
     const float sig = sigma_p[0], sd = sigma_d_p[0];
     const float sig2 = sig * sig, sd2 = sd * sd;
     if (tid < k) nidx[tid] = min(max(knn[((size_t)b * S + s) * k + tid], 0), N - 1);
     __syncthreads();
     const float *Fb = normed + (size_t)b * N * CH;
-    for (int e = tid; e < k * (CH / 4); e += 256) {
+    const int kp = (k + 1) & ~1;  // rows padded to even (zero features) for 2x2 blocking
+    for (int e = tid; e < kp * (CH / 4); e += 256) {
         const int a = e / (CH / 4), c4 = e % (CH / 4);
         *reinterpret_cast<f32x4 *>(&F[a * FSTR + 4 * c4]) =
-            *reinterpret_cast<const f32x4 *>(Fb + (size_t)nidx[a] * CH + 4 * c4);
+            (a < k) ? *reinterpret_cast<const f32x4 *>(Fb + (size_t)nidx[a] * CH + 4 * c4) : f32x4{0, 0, 0, 0};
     }
     for (int e = tid; e < k * 6; e += 256) {
         const int a = e / 6, c = e % 6;
@@ -224,57 +213,99 @@ __global__ __launch_bounds__(256) void nsm_power_kernel(const float *__restrict_
         P[a][c] = base[c % 3];
     }
     __syncthreads();
-    // local consistency (models/PointDSC.py:257-278)
-    for (int e = tid; e < k * k; e += 256) {
-        const int a = e / k, c = e % k;
-        float val = 0.0f;
-        if (a != c) {
-            const f32x4 *fa = reinterpret_cast<const f32x4 *>(&F[a * FSTR]);
-            const f32x4 *fc = reinterpret_cast<const f32x4 *>(&F[c * FSTR]);
-            f32x4 acc = {0, 0, 0, 0};
-#pragma unroll 8
-            for (int i = 0; i < CH / 4; ++i) {
-                const f32x4 x = fa[i], y = fc[i];
-                acc[0] = __builtin_fmaf(x[0], y[0], acc[0]);
-                acc[1] = __builtin_fmaf(x[1], y[1], acc[1]);
-                acc[2] = __builtin_fmaf(x[2], y[2], acc[2]);
-                acc[3] = __builtin_fmaf(x[3], y[3], acc[3]);
-            }
-            const float dot = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-            const float fm = fmaxf(1.0f - (1.0f - dot) / sig2, 0.0f);
-            float dx = P[a][0] - P[c][0], dy = P[a][1] - P[c][1], dz = P[a][2] - P[c][2];
-            const float ds = sqrtf((dx * dx + dy * dy) + dz * dz);
-            dx = P[a][3] - P[c][3];
-            dy = P[a][4] - P[c][4];
-            dz = P[a][5] - P[c][5];
-            const float dt = sqrtf((dx * dx + dy * dy) + dz * dz);
-            const float dd = ds - dt;
-            const float sm = fmaxf(1.0f - (dd * dd) / sd2, 0.0f);
-            val = fm * sm;
+    // local consistency (models/PointDSC.py:257-278).  The feature Gram matrix is
+    // symmetric: each thread owns one 2x2 block of its upper triangle (4 dot
+    // products sharing 4 row reads), and writes both mirrored entries.
+    const int nbk = kp / 2;
+    for (int t = tid; t < nbk * (nbk + 1) / 2; t += 256) {
+        int bi = 0, rem = t;
+        while (rem >= nbk - bi) {
+            rem -= nbk - bi;
+            ++bi;
         }
-        Tm[a][c] = val;
+        const int bj = bi + rem;
+        const int a0 = 2 * bi, c0 = 2 * bj;
+        const f32x4 *fa0 = reinterpret_cast<const f32x4 *>(&F[a0 * FSTR]);
+        const f32x4 *fa1 = reinterpret_cast<const f32x4 *>(&F[(a0 + 1) * FSTR]);
+        const f32x4 *fc0 = reinterpret_cast<const f32x4 *>(&F[c0 * FSTR]);
+        const f32x4 *fc1 = reinterpret_cast<const f32x4 *>(&F[(c0 + 1) * FSTR]);
+        f32x4 d00 = {0, 0, 0, 0}, d01 = d00, d10 = d00, d11 = d00;
+#pragma unroll 4
+        for (int i = 0; i < CH / 4; ++i) {
+            const f32x4 x0 = fa0[i], x1 = fa1[i], y0 = fc0[i], y1 = fc1[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                d00[e] = __builtin_fmaf(x0[e], y0[e], d00[e]);
+                d01[e] = __builtin_fmaf(x0[e], y1[e], d01[e]);
+                d10[e] = __builtin_fmaf(x1[e], y0[e], d10[e]);
+                d11[e] = __builtin_fmaf(x1[e], y1[e], d11[e]);
+            }
+        }
+        const float dots[4] = {(d00[0] + d00[1]) + (d00[2] + d00[3]), (d01[0] + d01[1]) + (d01[2] + d01[3]),
+                               (d10[0] + d10[1]) + (d10[2] + d10[3]), (d11[0] + d11[1]) + (d11[2] + d11[3])};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = a0 + (q >> 1), c = c0 + (q & 1);
+            if (a >= k || c >= k || a > c) continue;  // upper triangle (diagonal block: a <= c)
+            float val = 0.0f;
+            if (a != c) {
+                const float fm = fmaxf(1.0f - (1.0f - dots[q]) / sig2, 0.0f);  // :259
+                float dx = P[a][0] - P[c][0], dy = P[a][1] - P[c][1], dz = P[a][2] - P[c][2];
+                const float ds = sqrtf((dx * dx + dy * dy) + dz * dz);       // :268
+                dx = P[a][3] - P[c][3];
+                dy = P[a][4] - P[c][4];
+                dz = P[a][5] - P[c][5];
+                const float dt = sqrtf((dx * dx + dy * dy) + dz * dz);
+                const float dd = ds - dt;
+                const float sm = fmaxf(1.0f - (dd * dd) / sd2, 0.0f);        // :270
+                val = fm * sm;                                               // :277 (diag 0, :278)
+            }
+            Tb[a * k + c] = val;
+            Tb[c * k + a] = val;
+        }
     }
-    if (tid < KMAX) vbuf[tid] = 1.0f;
-    __syncthreads();
-    // power iteration (models/PointDSC.py:347-358), all T iterates, in wave 0
-    if (tid < 64) {
-        const int a = tid;
+}
+
+// nsm_iter: one WAVE per seed (4 seeds per workgroup) runs all T power
+// iterates (models/PointDSC.py:347-358): lane a keeps row a of T in registers,
+// v is broadcast from LDS 4 entries at a time.  hist[b][s][t][a] = iterate t+1;
+// bit t of the seed's flag word = allclose(v_{t+1}, v_t), AND-ed into pair_mask[b].
+__global__ __launch_bounds__(256) void nsm_iter_kernel(const float *__restrict__ Tg, int S, int k, int T,
+                                                       float *__restrict__ hist,
+                                                       unsigned *__restrict__ pair_mask) {
+    __shared__ __attribute__((aligned(16))) float vb[4][KMAX];
+    const int b = blockIdx.y, wave = threadIdx.x >> 6, a = threadIdx.x & 63;
+    const int s = blockIdx.x * 4 + wave;
+    if (s >= S) return;
+    float *vbuf = vb[wave];
+    vbuf[a] = 1.0f;
+    {
+        const float *Tb = Tg + ((size_t)b * S + s) * k * k;
+        float trow[KMAX];
+#pragma unroll
+        for (int c = 0; c < KMAX; ++c) trow[c] = (a < k && c < k) ? Tb[a * k + c] : 0.0f;
         float v = (a < k) ? 1.0f : 0.0f;
         unsigned flags = 0;
         float *hb = hist + ((size_t)b * S + s) * T * k;
         for (int t = 0; t < T; ++t) {
-            float nv = 0.0f;
-            if (a < k) {
-                for (int c = 0; c < k; ++c) nv = __builtin_fmaf(Tm[a][c], vbuf[c], nv);
+            float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int c = 0; c < KMAX; c += 4) {
+                const f32x4 vv = *reinterpret_cast<const f32x4 *>(&vbuf[c]);
+                acc[0] = __builtin_fmaf(trow[c], vv[0], acc[0]);
+                acc[1] = __builtin_fmaf(trow[c + 1], vv[1], acc[1]);
+                acc[2] = __builtin_fmaf(trow[c + 2], vv[2], acc[2]);
+                acc[3] = __builtin_fmaf(trow[c + 3], vv[3], acc[3]);
             }
+            float nv = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // (T v)_a  (bmm, :352)
             const float nrm = sqrtf(wave_sum(nv * nv));
-            nv = nv / (nrm + 1e-6f);
-            const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));
+            nv = nv / (nrm + 1e-6f);                              // :353
+            const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
             if (__all(close)) flags |= 1u << t;
             if (a < k) hb[(size_t)t * k + a] = nv;
             v = nv;
             __builtin_amdgcn_wave_barrier();
-            if (a < KMAX) vbuf[a] = nv;
+            vbuf[a] = nv;
             __builtin_amdgcn_wave_barrier();
         }
         if (a == 0) atomicAnd(&pair_mask[b], flags);
@@ -283,9 +314,11 @@ __global__ __launch_bounds__(256) void nsm_power_kernel(const float *__restrict_
 
 hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
                             int B, int N, int S, int k, int T, const float *sigma,
-                            const float *sigma_d, float *hist, unsigned *pair_mask, hipStream_t s) {
-    hipLaunchKernelGGL(nsm_power_kernel, dim3(S, B), dim3(256), 0, s, normed, src, tgt, knn, N, S, k,
-                       T, sigma, sigma_d, hist, pair_mask);
+                            const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), 0, s, normed, src, tgt, knn, N, S, k,
+                       sigma, sigma_d, Tg);
+    hipLaunchKernelGGL(nsm_iter_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, Tg, S, k, T, hist, pair_mask);
     return hipGetLastError();
 }
 
@@ -313,14 +346,68 @@ hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B
 }
 
 // ------------------------------------------------------------ a9 Kabsch
-// Finish a weighted Kabsch from its sums: centroids already formed, H given.
-// t = c_B - R c_A in fp32 as models/common.py:42 computes it.
+// Hypotheses (models/PointDSC.py:287-328) in three SIMD-friendly steps:
+//  1. kabsch_sums   one wave per seed: weighted centroids and H (wave reductions)
+//  2. kabsch_solve  one LANE per seed: fp64 3x3 rotation + t (64 solves per wave)
+//  3. count_inliers one workgroup per HS seeds: every correspondence's residual
+//                   under all HS hypotheses (src/tgt read once per HS seeds)
+constexpr int HSUM = 15;  // H[9], cA[3], cB[3]
+constexpr int HS = 8;     // seeds per count_inliers workgroup
+
+__global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restrict__ src,
+                                                          const float *__restrict__ tgt,
+                                                          const int *__restrict__ knn,
+                                                          const float *__restrict__ weights, int N,
+                                                          int S, int k, float *__restrict__ sums) {
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= S) return;
+    const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
+    float w = 0, ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
+    if (lane < k) {
+        const int j = min(max(knn[((size_t)b * S + s) * k + lane], 0), N - 1);
+        w = weights[((size_t)b * S + s) * k + lane];
+        ax = sb[3 * j];
+        ay = sb[3 * j + 1];
+        az = sb[3 * j + 2];
+        bx = tb[3 * j];
+        by = tb[3 * j + 1];
+        bz = tb[3 * j + 2];
+    }
+    // centroid = sum(A * w) / (sum(w) + 1e-6)  (models/common.py:24-25)
+    const float den = wave_sum(w) + 1e-6f;
+    const float cA0 = wave_sum(ax * w) / den, cA1 = wave_sum(ay * w) / den, cA2 = wave_sum(az * w) / den;
+    const float cB0 = wave_sum(bx * w) / den, cB1 = wave_sum(by * w) / den, cB2 = wave_sum(bz * w) / den;
+    const float am[3] = {ax - cA0, ay - cA1, az - cA2};
+    const float bm[3] = {bx - cB0, by - cB1, bz - cB2};
+    float out = 0.0f;  // lane e < 15 keeps sums[e]
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+            const float h = wave_sum((am[i] * w) * bm[jj]);  // H = Am^T diag(w) Bm (:33)
+            if (lane == 3 * i + jj) out = h;
+        }
+    if (lane == 9) out = cA0;
+    if (lane == 10) out = cA1;
+    if (lane == 11) out = cA2;
+    if (lane == 12) out = cB0;
+    if (lane == 13) out = cB1;
+    if (lane == 14) out = cB2;
+    if (lane < HSUM) sums[((size_t)b * S + s) * HSUM + lane] = out;
+}
+
+// Finish a weighted Kabsch from its sums: t = c_B - R c_A in fp32 as
+// models/common.py:42 computes it; T row-major 4x4.
 PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[3], float *T) {
     double Hd[9], Rd[9];
+#pragma unroll
     for (int i = 0; i < 9; ++i) Hd[i] = H[i];
     kabsch_rotation(Hd, Rd);
     float R[9];
+#pragma unroll
     for (int i = 0; i < 9; ++i) R[i] = (float)Rd[i];
+#pragma unroll
     for (int r = 0; r < 3; ++r) {
         T[4 * r + 0] = R[3 * r + 0];
         T[4 * r + 1] = R[3 * r + 1];
@@ -333,71 +420,66 @@ PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[
     T[15] = 1.0f;
 }
 
-// Hypothesis per seed: Kabsch on its k neighbours (wave 0), then count inliers
-// over all N correspondences (all waves).  models/PointDSC.py:287-328.
-__global__ __launch_bounds__(256) void hypotheses_kernel(const float *__restrict__ src,
-                                                         const float *__restrict__ tgt,
-                                                         const int *__restrict__ knn,
-                                                         const float *__restrict__ weights, int N,
-                                                         int S, int k, float tau,
-                                                         float *__restrict__ seed_trans,
-                                                         int *__restrict__ counts) {
-    __shared__ float Ts[16];
-    __shared__ int wcnt[4];
-    const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__global__ __launch_bounds__(64) void kabsch_solve_kernel(const float *__restrict__ sums, int n,
+                                                          float *__restrict__ trans) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const float *p = sums + (size_t)i * HSUM;
+    float H[9], cA[3], cB[3], T[16];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) H[e] = p[e];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+        cA[e] = p[9 + e];
+        cB[e] = p[12 + e];
+    }
+    kabsch_finish(H, cA, cB, T);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) trans[(size_t)i * 16 + e] = T[e];
+}
+
+__global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restrict__ src,
+                                                            const float *__restrict__ tgt,
+                                                            const float *__restrict__ seed_trans,
+                                                            int N, int S, float tau,
+                                                            int *__restrict__ counts) {
+    __shared__ float Ts[HS][12];
+    __shared__ int wc[4][HS];
+    const int b = blockIdx.y, s0 = blockIdx.x * HS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ns = min(HS, S - s0);
+    if (tid < HS * 12) {
+        const int q = tid / 12, e = tid % 12;
+        Ts[q][e] = (q < ns) ? seed_trans[((size_t)b * S + s0 + q) * 16 + e] : 0.0f;
+    }
+    __syncthreads();
     const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
-    if (wave == 0) {
-        float w = 0, ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
-        if (lane < k) {
-            const int j = min(max(knn[((size_t)b * S + s) * k + lane], 0), N - 1);
-            w = weights[((size_t)b * S + s) * k + lane];
-            ax = sb[3 * j];
-            ay = sb[3 * j + 1];
-            az = sb[3 * j + 2];
-            bx = tb[3 * j];
-            by = tb[3 * j + 1];
-            bz = tb[3 * j + 2];
-        }
-        const float den = wave_sum(w) + 1e-6f;
-        const float cA[3] = {wave_sum(ax * w) / den, wave_sum(ay * w) / den, wave_sum(az * w) / den};
-        const float cB[3] = {wave_sum(bx * w) / den, wave_sum(by * w) / den, wave_sum(bz * w) / den};
-        const float am[3] = {ax - cA[0], ay - cA[1], az - cA[2]};
-        const float bm[3] = {bx - cB[0], by - cB[1], bz - cB[2]};
-        float H[9];
+    int c[HS];
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 3; ++jj) H[3 * i + jj] = wave_sum((am[i] * w) * bm[jj]);
-        if (lane == 0) {
-            float T[16];
-            kabsch_finish(H, cA, cB, T);
-            for (int e = 0; e < 16; ++e) {
-                Ts[e] = T[e];
-                seed_trans[((size_t)b * S + s) * 16 + e] = T[e];
-            }
-        }
-    }
-    __syncthreads();
-    float T[12];
-#pragma unroll
-    for (int e = 0; e < 12; ++e) T[e] = Ts[e];
-    int c = 0;
+    for (int q = 0; q < HS; ++q) c[q] = 0;
     for (int n = tid; n < N; n += 256) {
-        const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
-                                  tb[3 * n + 2]);
-        c += L2 < tau;
+        const float x = sb[3 * n], y = sb[3 * n + 1], z = sb[3 * n + 2];
+        const float tx = tb[3 * n], ty = tb[3 * n + 1], tz = tb[3 * n + 2];
+#pragma unroll
+        for (int q = 0; q < HS; ++q) c[q] += residual(Ts[q], x, y, z, tx, ty, tz) < tau;  // (:327-328)
     }
-    c = wave_sum(c);
-    if (lane == 0) wcnt[wave] = c;
+#pragma unroll
+    for (int q = 0; q < HS; ++q) {
+        const int v = wave_sum(c[q]);
+        if (lane == 0) wc[wave][q] = v;
+    }
     __syncthreads();
-    if (tid == 0) counts[(size_t)b * S + s] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (tid < ns) counts[(size_t)b * S + s0 + tid] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
 }
 
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(hypotheses_kernel, dim3(S, B), dim3(256), 0, s, src, tgt, knn, weights, N, S, k,
-                       tau, seed_trans, counts);
+                             float *sums, hipStream_t s) {
+    hipLaunchKernelGGL(kabsch_sums_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, src, tgt, knn, weights,
+                       N, S, k, sums);
+    const int n = B * S;
+    hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, seed_trans);
+    hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
+                       seed_trans, N, S, tau, counts);
     return hipGetLastError();
 }
 
@@ -460,7 +542,7 @@ hipError_t launch_select_best(const float *src, const float *tgt, const float *s
 }
 
 // --------------------------------------------------- block-wide Kabsch
-constexpr int RB = 1024;  // threads per refinement / rigid workgroup
+constexpr int RB = 256;  // threads per refinement / rigid workgroup (register room for the fp64 SVD)
 constexpr int RW = RB / 64;
 
 template <int NV>

@@ -69,106 +69,113 @@ PDSC_DEV float residual(const float *T, float x, float y, float z, float tx, flo
 // models/common.py:36-41).  R = V diag(1,1,det(V U^T)) U^T with H = U S V^T.
 // The result is independent of the SVD's sign choices: with u3 = u1 x u2,
 // R = v1 u1^T + v2 u2^T + det(V) v3 u3^T.
+// Written with named scalars only (no runtime-indexed arrays -> no scratch),
+// so it runs SIMD-parallel when every lane solves its own H.
 // ---------------------------------------------------------------------------
-PDSC_DEV void jacobi_eig3(double A[3][3], double V[3][3]) {
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 12; ++sweep) {
-        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
-        const double dia = A[0][0] * A[0][0] + A[1][1] * A[1][1] + A[2][2] * A[2][2];
-        if (off <= 1e-30 * dia || off == 0.0) break;
-        for (int p = 0; p < 2; ++p) {
-            for (int q = p + 1; q < 3; ++q) {
-                const double apq = A[p][q];
-                if (apq == 0.0) continue;
-                const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < 3; ++k) {  // A = J^T A J
-                    const double akp = A[k][p], akq = A[k][q];
-                    A[k][p] = c * akp - s * akq;
-                    A[k][q] = s * akp + c * akq;
-                }
-                for (int k = 0; k < 3; ++k) {
-                    const double apk = A[p][k], aqk = A[q][k];
-                    A[p][k] = c * apk - s * aqk;
-                    A[q][k] = s * apk + c * aqk;
-                }
-                for (int k = 0; k < 3; ++k) {
-                    const double vkp = V[k][p], vkq = V[k][q];
-                    V[k][p] = c * vkp - s * vkq;
-                    V[k][q] = s * vkp + c * vkq;
-                }
-            }
-        }
+struct D3 {
+    double x, y, z;
+};
+PDSC_DEV D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+PDSC_DEV double dot3(const D3 &a, const D3 &b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PDSC_DEV D3 cross3(const D3 &a, const D3 &b) {
+    return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+PDSC_DEV double normalize3(D3 &a) {
+    const double n = sqrt(dot3(a, a));
+    if (n > 0) {
+        const double inv = 1.0 / n;
+        a.x *= inv;
+        a.y *= inv;
+        a.z *= inv;
+    }
+    return n;
+}
+PDSC_DEV D3 orthogonal3(const D3 &a) {  // a unit vector orthogonal to a (deterministic)
+    const double ax = fabs(a.x), ay = fabs(a.y), az = fabs(a.z);
+    D3 e = (ax <= ay && ax <= az) ? d3(1, 0, 0) : (ay <= az ? d3(0, 1, 0) : d3(0, 0, 1));
+    D3 o = cross3(a, e);
+    normalize3(o);
+    return o;
+}
+
+// One Jacobi rotation zeroing a_pq of a symmetric 3x3 (r = the third index);
+// vp, vq = eigenvector columns p and q.
+PDSC_DEV void jrot(double &app, double &aqq, double &apq, double &arp, double &arq, D3 &vp, D3 &vq) {
+    if (apq == 0.0) return;
+    const double theta = (aqq - app) / (2.0 * apq);
+    const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+    const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+    app -= t * apq;
+    aqq += t * apq;
+    apq = 0.0;
+    const double rp = arp, rq = arq;
+    arp = c * rp - s * rq;
+    arq = s * rp + c * rq;
+    const D3 p0 = vp, q0 = vq;
+    vp = d3(c * p0.x - s * q0.x, c * p0.y - s * q0.y, c * p0.z - s * q0.z);
+    vq = d3(s * p0.x + c * q0.x, s * p0.y + c * q0.y, s * p0.z + c * q0.z);
+}
+
+PDSC_DEV void cswap(double &la, double &lb, D3 &va, D3 &vb) {  // order (la, va) >= (lb, vb)
+    if (la < lb) {
+        const double t = la;
+        la = lb;
+        lb = t;
+        const D3 tv = va;
+        va = vb;
+        vb = tv;
     }
 }
 
-PDSC_DEV void cross3(const double *a, const double *b, double *c) {
-    c[0] = a[1] * b[2] - a[2] * b[1];
-    c[1] = a[2] * b[0] - a[0] * b[2];
-    c[2] = a[0] * b[1] - a[1] * b[0];
-}
-
-PDSC_DEV double normalize3(double *a) {
-    const double n = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-    if (n > 0) { a[0] /= n; a[1] /= n; a[2] /= n; }
-    return n;
-}
-
-// Any unit vector orthogonal to a (deterministic).
-PDSC_DEV void orthogonal3(const double *a, double *o) {
-    const double e[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
-    int best = 0;
-    double bm = fabs(a[0]);
-    if (fabs(a[1]) < bm) { best = 1; bm = fabs(a[1]); }
-    if (fabs(a[2]) < bm) { best = 2; }
-    cross3(a, e[best], o);
-    normalize3(o);
-}
-
-// H (row-major 3x3, H[i][j] = sum w Am_i Bm_j) -> R (row-major, fp64).
+// H row-major (H[i][j] = sum w Am_i Bm_j) -> R row-major.
 PDSC_DEV void kabsch_rotation(const double H[9], double R[9]) {
-    double A[3][3], V[3][3];
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            double s = 0;
-            for (int k = 0; k < 3; ++k) s += H[k * 3 + i] * H[k * 3 + j];  // H^T H
-            A[i][j] = s;
-        }
-    jacobi_eig3(A, V);
-    // sort eigenpairs descending
-    int ord[3] = {0, 1, 2};
-    double lam[3] = {A[0][0], A[1][1], A[2][2]};
-    for (int i = 0; i < 2; ++i)
-        for (int j = 0; j < 2 - i; ++j)
-            if (lam[ord[j]] < lam[ord[j + 1]]) { int t = ord[j]; ord[j] = ord[j + 1]; ord[j + 1] = t; }
-    double v[3][3], u[3][3];  // v[i] = i-th right singular vector
-    for (int i = 0; i < 3; ++i)
-        for (int k = 0; k < 3; ++k) v[i][k] = V[k][ord[i]];
+    // A = H^T H (symmetric)
+    double a00 = H[0] * H[0] + H[3] * H[3] + H[6] * H[6];
+    double a11 = H[1] * H[1] + H[4] * H[4] + H[7] * H[7];
+    double a22 = H[2] * H[2] + H[5] * H[5] + H[8] * H[8];
+    double a01 = H[0] * H[1] + H[3] * H[4] + H[6] * H[7];
+    double a02 = H[0] * H[2] + H[3] * H[5] + H[6] * H[8];
+    double a12 = H[1] * H[2] + H[4] * H[5] + H[7] * H[8];
+    D3 v0 = d3(1, 0, 0), v1 = d3(0, 1, 0), v2 = d3(0, 0, 1);  // eigenvector columns
+    for (int sweep = 0; sweep < 10; ++sweep) {
+        const double off = a01 * a01 + a02 * a02 + a12 * a12;
+        const double dia = a00 * a00 + a11 * a11 + a22 * a22;
+        // off-diagonal below ~1e-13 of the diagonal: far beyond the fp32 result's needs
+        if (off <= 1e-26 * dia || off == 0.0) break;
+        jrot(a00, a11, a01, a02, a12, v0, v1);  // (p,q,r) = (0,1,2)
+        jrot(a00, a22, a02, a01, a12, v0, v2);  // (0,2,1)
+        jrot(a11, a22, a12, a01, a02, v1, v2);  // (1,2,0)
+    }
+    cswap(a00, a11, v0, v1);
+    cswap(a00, a22, v0, v2);
+    cswap(a11, a22, v1, v2);
     double scale = 0;
     for (int i = 0; i < 9; ++i) scale = fmax(scale, fabs(H[i]));
     if (!(scale > 0)) {  // H == 0: LAPACK returns U = V = I -> R = I
         for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    for (int i = 0; i < 2; ++i)
-        for (int r = 0; r < 3; ++r) u[i][r] = H[r * 3 + 0] * v[i][0] + H[r * 3 + 1] * v[i][1] + H[r * 3 + 2] * v[i][2];
-    const double n0 = normalize3(u[0]);
-    if (!(n0 > 1e-300)) orthogonal3(v[0], u[0]);
-    // Gram-Schmidt u1 against u0 for robustness
-    double d01 = u[1][0] * u[0][0] + u[1][1] * u[0][1] + u[1][2] * u[0][2];
-    for (int r = 0; r < 3; ++r) u[1][r] -= d01 * u[0][r];
-    const double n1 = normalize3(u[1]);
-    if (!(n1 > 1e-12 * n0)) orthogonal3(u[0], u[1]);
-    cross3(u[0], u[1], u[2]);
-    double c12[3];
-    cross3(v[1], v[2], c12);
-    const double detV = v[0][0] * c12[0] + v[0][1] * c12[1] + v[0][2] * c12[2];
-    const double d = detV < 0 ? -1.0 : 1.0;
-    for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b)
-            R[a * 3 + b] = v[0][a] * u[0][b] + v[1][a] * u[1][b] + d * v[2][a] * u[2][b];
+    D3 u0 = d3(H[0] * v0.x + H[1] * v0.y + H[2] * v0.z, H[3] * v0.x + H[4] * v0.y + H[5] * v0.z,
+               H[6] * v0.x + H[7] * v0.y + H[8] * v0.z);
+    D3 u1 = d3(H[0] * v1.x + H[1] * v1.y + H[2] * v1.z, H[3] * v1.x + H[4] * v1.y + H[5] * v1.z,
+               H[6] * v1.x + H[7] * v1.y + H[8] * v1.z);
+    const double n0 = normalize3(u0);
+    if (!(n0 > 1e-300)) u0 = orthogonal3(v0);
+    const double d01 = dot3(u1, u0);  // Gram-Schmidt u1 against u0 for robustness
+    u1 = d3(u1.x - d01 * u0.x, u1.y - d01 * u0.y, u1.z - d01 * u0.z);
+    const double n1 = normalize3(u1);
+    if (!(n1 > 1e-12 * n0)) u1 = orthogonal3(u0);
+    const D3 u2 = cross3(u0, u1);
+    const double d = dot3(v0, cross3(v1, v2)) < 0 ? -1.0 : 1.0;  // det(V); det(U) = +1
+    R[0] = v0.x * u0.x + v1.x * u1.x + d * v2.x * u2.x;
+    R[1] = v0.x * u0.y + v1.x * u1.y + d * v2.x * u2.y;
+    R[2] = v0.x * u0.z + v1.x * u1.z + d * v2.x * u2.z;
+    R[3] = v0.y * u0.x + v1.y * u1.x + d * v2.y * u2.x;
+    R[4] = v0.y * u0.y + v1.y * u1.y + d * v2.y * u2.y;
+    R[5] = v0.y * u0.z + v1.y * u1.z + d * v2.y * u2.z;
+    R[6] = v0.z * u0.x + v1.z * u1.x + d * v2.z * u2.x;
+    R[7] = v0.z * u0.y + v1.z * u1.y + d * v2.z * u2.y;
+    R[8] = v0.z * u0.z + v1.z * u1.z + d * v2.z * u2.z;
 }
 
 }  // namespace pdsc

@@ -11,7 +11,7 @@ constexpr int CH2 = CH / 2;   // fc_message hidden width (models/PointDSC.py:12-
 constexpr int CLS = 32;       // classifier hidden width (models/PointDSC.py:107-113)
 constexpr int QB = 128;       // queries per attention workgroup (4 waves x 32)
 constexpr int KT = 32;        // keys per attention tile
-constexpr int PT = 32;        // points per pointwise workgroup
+constexpr int PT = 64;        // points per pointwise workgroup
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
@@ -123,14 +123,17 @@ hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, in
 hipError_t launch_knn_dist(const float *normed, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s);
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s);
+// Tg: scratch [B][S][k][k]
 hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
                             int B, int N, int S, int k, int T, const float *sigma,
-                            const float *sigma_d, float *hist, unsigned *pair_mask, hipStream_t s);
+                            const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
+                            hipStream_t s);
 hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B, int S, int k, int T,
                              float *weights, int *iters_used, hipStream_t s);
+// sums: scratch [B][S][15]
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             hipStream_t s);
+                             float *sums, hipStream_t s);
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
                               const int *counts, int B, int N, int S, float tau, float *fitness,
                               int *best, float *trans, float *labels, hipStream_t s);

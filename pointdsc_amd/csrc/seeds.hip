@@ -13,11 +13,18 @@
 
 namespace pdsc {
 
+// A workgroup owns 64 rows i (lane = i) and sweeps all j in 256-point LDS
+// tiles; its four waves take disjoint quarters of each tile, so a pair of
+// N = 1000 runs on 16 workgroups instead of 4.  Partial results meet in LDS.
+constexpr int SQ = 64;  // rows per workgroup
+
 __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict__ src,
                                                         const float *__restrict__ conf, int N,
                                                         float R, float *__restrict__ lm) {
-    __shared__ float sx[256], sy[256], sz[256], sc[256];
-    const int b = blockIdx.y, tid = threadIdx.x, i = blockIdx.x * 256 + tid;
+    __shared__ f32x4 tile[256];
+    __shared__ int part[4][SQ];
+    const int b = blockIdx.y, tid = threadIdx.x, q = tid >> 6, il = tid & 63;
+    const int i = blockIdx.x * SQ + il;
     src += (size_t)b * N * 3;
     conf += (size_t)b * N;
     float xi = 0, yi = 0, zi = 0, ci = 0;
@@ -31,56 +38,63 @@ __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict_
     for (int j0 = 0; j0 < N; j0 += 256) {
         __syncthreads();
         const int j = j0 + tid;
-        if (j < N) {
-            sx[tid] = src[3 * j];
-            sy[tid] = src[3 * j + 1];
-            sz[tid] = src[3 * j + 2];
-            sc[tid] = conf[j];
-        }
+        // padding points never violate: conf -inf
+        tile[tid] = (j < N) ? f32x4{src[3 * j], src[3 * j + 1], src[3 * j + 2], conf[j]}
+                            : f32x4{0.0f, 0.0f, 0.0f, -INFINITY};
         __syncthreads();
-        const int cnt = min(256, N - j0);
-        for (int jj = 0; jj < cnt; ++jj) {
-            if (ci < sc[jj]) {  // relation false unless the pair is out of radius
-                const float d = pdist3(xi, yi, zi, sx[jj], sy[jj], sz[jj]);
+#pragma unroll 4
+        for (int jj = q * 64; jj < q * 64 + 64; ++jj) {
+            const f32x4 pj = tile[jj];
+            if (ci < pj[3]) {  // relation false unless the pair is out of radius
+                const float d = pdist3(xi, yi, zi, pj[0], pj[1], pj[2]);
                 if (!(d >= R)) ok = false;
             }
         }
     }
-    if (i < N) lm[(size_t)b * N + i] = ok ? 1.0f : 0.0f;
+    part[q][il] = ok;
+    __syncthreads();
+    if (q == 0 && i < N) lm[(size_t)b * N + i] = (part[0][il] & part[1][il] & part[2][il] & part[3][il]) ? 1.0f : 0.0f;
 }
 
 __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict__ conf,
                                                         const float *__restrict__ lm, int N, int S,
                                                         int *__restrict__ seeds) {
     __shared__ float ss[256];
-    const int b = blockIdx.y, tid = threadIdx.x, i = blockIdx.x * 256 + tid;
+    __shared__ int part[4][SQ];
+    const int b = blockIdx.y, tid = threadIdx.x, q = tid >> 6, il = tid & 63;
+    const int i = blockIdx.x * SQ + il;
     conf += (size_t)b * N;
     lm += (size_t)b * N;
     const float si = (i < N) ? conf[i] * lm[i] : 0.0f;  // scores * is_local_max (:217)
     int rank = 0;
     for (int j0 = 0; j0 < N; j0 += 256) {
         __syncthreads();
-        if (j0 + tid < N) ss[tid] = conf[j0 + tid] * lm[j0 + tid];
+        ss[tid] = (j0 + tid < N) ? conf[j0 + tid] * lm[j0 + tid] : -INFINITY;
         __syncthreads();
-        const int cnt = min(256, N - j0);
-        for (int jj = 0; jj < cnt; ++jj) {
+#pragma unroll 8
+        for (int jj = q * 64; jj < q * 64 + 64; ++jj) {
             const float sj = ss[jj];
             rank += (sj > si) || (sj == si && j0 + jj < i);
         }
     }
-    if (i < N && rank < S) seeds[(size_t)b * S + rank] = i;
+    part[q][il] = rank;
+    __syncthreads();
+    if (q == 0 && i < N) {
+        rank = part[0][il] + part[1][il] + part[2][il] + part[3][il];
+        if (rank < S) seeds[(size_t)b * S + rank] = i;
+    }
 }
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s) {
-    hipLaunchKernelGGL(local_max_kernel, dim3((N + 255) / 256, B), dim3(256), 0, s, src, conf, N,
+    hipLaunchKernelGGL(local_max_kernel, dim3((N + SQ - 1) / SQ, B), dim3(256), 0, s, src, conf, N,
                        radius, lm);
     return hipGetLastError();
 }
 
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
                             hipStream_t s) {
-    hipLaunchKernelGGL(seed_rank_kernel, dim3((N + 255) / 256, B), dim3(256), 0, s, conf, lm, N, S,
+    hipLaunchKernelGGL(seed_rank_kernel, dim3((N + SQ - 1) / SQ, B), dim3(256), 0, s, conf, lm, N, S,
                        seeds);
     return hipGetLastError();
 }

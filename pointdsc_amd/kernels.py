@@ -175,9 +175,12 @@ def seed_hypotheses(src, tgt, knn, weights, tau: float):
     best = torch.empty((B,), dtype=torch.int32, device=dev)
     trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
     labels = torch.empty((B, N), dtype=torch.float32, device=dev)
-    check(_lib.load().pdsc_seed_hypotheses(_p(src), _p(tgt), _p(knn), _p(weights), B, N, S, k, float(tau),
-                                           _p(seed_trans), _p(fitness), _p(best), _p(trans), _p(labels),
-                                           _stream(dev)), "pdsc_seed_hypotheses")
+    L = _lib.load()
+    nb = L.pdsc_seed_hypotheses_workspace_bytes(B, S)
+    ws = _workspace(nb, dev)
+    check(L.pdsc_seed_hypotheses(_p(src), _p(tgt), _p(knn), _p(weights), B, N, S, k, float(tau),
+                                 _p(seed_trans), _p(fitness), _p(best), _p(trans), _p(labels), _p(ws), nb,
+                                 _stream(dev)), "pdsc_seed_hypotheses")
     return seed_trans, fitness, best, trans, labels
 
 
