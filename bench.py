@@ -13,6 +13,11 @@ Prints ONE JSON line (rank 0).  Also measured live with HIP events on the
 stream the kernels run on:
   roofline      -- the dominant kernel (SCNonlocal attention), fp32 MFMA bound
   roofline_hbm  -- the a1 compatibility kernel, HBM-write bound
+  roofline_path -- SURVEY 8(d)'s target: the compat + seed-kNN + NSM power-iteration
+                   stages at N=5000 (stage events inside the forward), HBM bound,
+                   priced with the algorithmic bytes B(N) = 24N + 4N^2 + S*k*(C+6)*4 + 4*S*k
+  stages        -- per-stage ms of the headline forward (pdsc_forward_timing events)
+  single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph
   cpu_baseline  -- the CPU oracle (oracle/, numpy + C) on a bounded sample
 """
 import argparse
@@ -46,7 +51,52 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--path-n", type=int, default=5000, help="N of the compat+NSM path roofline (0 = skip)")
+    ap.add_argument("--path-pairs", type=int, default=8)
     return ap.parse_args()
+
+
+STAGES = ["compat", "encoder", "seeds", "seed_knn", "nsm", "hypotheses", "post_refine"]
+
+
+class EventPool:
+    """A flat array of hipEvent_t for libpdsc's pdsc_forward_timing hook."""
+
+    def __init__(self, n):
+        import ctypes
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.n = n
+        self.ev = (ctypes.c_void_p * n)()
+        for i in range(n):
+            e = ctypes.c_void_p()
+            assert self.hip.hipEventCreate(ctypes.byref(e)) == 0
+            self.ev[i] = e.value
+        self.count = ctypes.c_int32(0)
+
+    def ms(self, a, b):
+        out = self.ct.c_float()
+        assert self.hip.hipEventElapsedTime(self.ct.byref(out), self.ct.c_void_p(self.ev[a]),
+                                            self.ct.c_void_p(self.ev[b])) == 0
+        return out.value
+
+    def stage_means(self):
+        """{stage: mean ms} over the forwards recorded so far."""
+        per = len(STAGES) + 1
+        calls = self.count.value // per
+        out = {}
+        for j, name in enumerate(STAGES):
+            out[name] = sum(self.ms(c * per + j, c * per + j + 1) for c in range(calls)) / max(calls, 1)
+        return out, calls
+
+    def __del__(self):
+        for i in range(self.n):
+            self.hip.hipEventDestroy(self.ct.c_void_p(self.ev[i]))
+
+
+def path_bytes(N, S, k, C=128):
+    """algorithmic HBM bytes of compat + power-iteration path for one pair."""
+    return 24.0 * N + 4.0 * N * N + S * k * (C + 6) * 4.0 + 4.0 * S * k
 
 
 class HipEvents:
@@ -138,6 +188,8 @@ def main():
     evs = HipEvents(args.steps * 12)
     _lib.check(L.pdsc_attention_timing(evs.start, evs.stop, evs.n, ctypes.byref(evs.count)),
                "pdsc_attention_timing")
+    sev = EventPool(args.steps * (len(STAGES) + 1))
+    _lib.check(L.pdsc_forward_timing(sev.ev, sev.n, ctypes.byref(sev.count)), "pdsc_forward_timing")
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -147,6 +199,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     L.pdsc_attention_timing(None, None, 0, None)
+    L.pdsc_forward_timing(None, 0, None)
     att_times = [evs.elapsed_ms(i) for i in range(evs.count.value)]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -187,6 +240,53 @@ def main():
                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(cach / PEAK_HBM_GBS, 4),
                         "traffic": None, "launch_ms": round(c_ms, 4), "bytes_per_launch": cbytes}
 
+        stage_ms, _ = sev.stage_means()
+        stages = {k: round(v, 4) for k, v in stage_ms.items()}
+
+        # ---- SURVEY 8(d) target: compat + seed kNN + NSM stages at N = path_n
+        roofline_path = None
+        if args.path_n > 0:
+            P5, N5 = args.path_pairs, args.path_n
+            d5 = synthetic_batch(P5, N5, seed=5000 + rank, preset=args.preset)
+            c5, s5, t5 = (torch.from_numpy(d5[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+            plan5 = kernels.ForwardPlan(cfg, packed, P5, N5, dev)
+            for _ in range(2):
+                plan5.run(c5, s5, t5)
+            reps = 5
+            ev5 = EventPool(reps * (len(STAGES) + 1))
+            L.pdsc_forward_timing(ev5.ev, ev5.n, ctypes.byref(ev5.count))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                plan5.run(c5, s5, t5)
+            torch.cuda.synchronize(dev)
+            fwd5 = (time.perf_counter() - t0) / reps
+            L.pdsc_forward_timing(None, 0, None)
+            st5, _ = ev5.stage_means()
+            S5, k5 = int(N5 * 0.1), min(40, N5 - 1)
+            pb = P5 * path_bytes(N5, S5, k5)
+            t_path = st5["compat"] + st5["seed_knn"] + st5["nsm"]
+            ach = pb / (t_path * 1e-3) / 1e9
+            roofline_path = {"stages": "compat + seed_knn + nsm", "bound": "hbm", "achieved": round(ach, 1),
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+                             "traffic": None, "num_corr": N5, "pairs": P5, "path_ms": round(t_path, 4),
+                             "bytes_per_pair": path_bytes(N5, S5, k5),
+                             "stage_ms": {k: round(v, 4) for k, v in st5.items()},
+                             "forward_ms": round(fwd5 * 1e3, 3),
+                             "correspondences_per_s": round(P5 * N5 / fwd5, 1)}
+            del plan5, c5, s5, t5
+
+        # ---- configs[1] literally: a single N pair per forward (latency), eager and graph-replayed
+        d1 = synthetic_batch(1, N, seed=7000 + rank, preset=args.preset)
+        c1, s1, t1 = (torch.from_numpy(d1[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+        plan1 = kernels.ForwardPlan(cfg, packed, 1, N, dev)
+        e_ms = event_time(lambda: plan1.run(c1, s1, t1), 20, stream)
+        plan1.capture(c1, s1, t1)
+        g_ms = event_time(lambda: plan1.run(c1, s1, t1), 50, stream)
+        single = {"num_corr": N, "eager_ms": round(e_ms, 4), "graph_ms": round(g_ms, 4),
+                  "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1)}
+        del plan1
+
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             from oracle import pdsc_oracle as O
@@ -220,7 +320,8 @@ def main():
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
             "synthetic_recall": recall,
-            "roofline": roofline, "roofline_hbm": roofline_hbm, "cpu_baseline": cpu,
+            "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
+            "stages_ms": stages, "single_pair": single, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

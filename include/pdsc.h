@@ -110,6 +110,14 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nspl
  * Pass capacity 0 to disable.  The caller owns the events and the counter.   */
 int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_events, int32_t capacity,
                               int32_t *count);
+/* Measurement hook (no reference counterpart): every pdsc_forward_testing
+ * call from the calling thread records PDSC_FORWARD_STAGES + 1 events on its
+ * stream -- events[c + 0] before a1, then one after each stage in the order
+ * a1 compat, a2-a4 encoder, a5 seeds, a6 seed kNN, a7-a8 NSM, a9-a10
+ * hypotheses+verification, a11 post-refinement -- with c = *count, then
+ * *count += 8, while *count + 8 <= capacity.  Capacity 0 disables.           */
+#define PDSC_FORWARD_STAGES 7
+int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *count);
 int32_t pdsc_attention_partials_f32(const float *q_pad, const float *k_pad, const float *v_pad,
                                     const float *M, int32_t B, int32_t N, float *opart, float *ml,
                                     pdsc_stream_t stream);

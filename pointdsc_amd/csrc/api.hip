@@ -20,6 +20,10 @@ thread_local std::string g_name;
 thread_local hipEvent_t *g_tstart = nullptr, *g_tstop = nullptr;
 thread_local int g_tcap = 0;
 thread_local int32_t *g_tcount = nullptr;
+// pdsc_forward_timing: PDSC_FORWARD_STAGES + 1 events per forward call
+thread_local hipEvent_t *g_fev = nullptr;
+thread_local int g_fcap = 0;
+thread_local int32_t *g_fcount = nullptr;
 
 int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -344,6 +348,14 @@ int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_event
     return PDSC_OK;
 }
 
+int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *count) {
+    if (capacity > 0 && (!events || !count)) return fail(PDSC_ERR_ARG, "null events/count with capacity %d", capacity);
+    g_fev = reinterpret_cast<hipEvent_t *>(const_cast<void **>(events));
+    g_fcap = capacity;
+    g_fcount = count;
+    return PDSC_OK;
+}
+
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit) {
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
@@ -478,27 +490,41 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     const FwdBufs f = carve_forward(c, d);
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
     const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
+    const bool timed = g_fcap > 0 && g_fcount && *g_fcount + PDSC_FORWARD_STAGES + 1 <= g_fcap;
+    hipEvent_t *ev = timed ? g_fev + *g_fcount : nullptr;
+    if (timed) *g_fcount += PDSC_FORWARD_STAGES + 1;
+#define STAGE(i) \
+    if (ev) HIPCHK(hipEventRecord(ev[i], s))
+    STAGE(0);
     // a1 (:150-153)
     HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    STAGE(1);
     // a2-a4 (:155-156, :171)
     RET_IF(run_encoder(lay, packed, corr_pos, f.M, d, f.enc, nullptr, f.normed, f.conf, s));
+    STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s));
     HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
+    STAGE(3);
     // a6 (:250-252)
     HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
     HIPCHK(launch_knn_dist(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
     HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
+    STAGE(4);
     // a7-a8 (:257-282)
     RET_IF(run_nsm(f.normed, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
                    nullptr, s));
+    STAGE(5);
     // a9-a10 (:287-335)
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
                              f.seed_trans, f.counts, f.hsums, s));
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
                               nullptr, nullptr, final_trans, final_labels, s));
+    STAGE(6);
     // a11 (:186, :403-438)
     HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s));
+    STAGE(7);
+#undef STAGE
     if (conf_out) HIPCHK(hipMemcpyAsync(conf_out, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
     if (seeds_out)
         HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));

@@ -25,9 +25,9 @@ namespace pdsc {
 constexpr int A_KSTR = CH + 4;  // K row stride in LDS: conflict-free ds_read_b128 columns
 constexpr int A_VSTR = CH;
 
-template <int NW, int KTS>
+template <int NW, int KTS, bool GLDS = false>
 constexpr size_t attention_lds_bytes() {
-    return (size_t)2 * KTS * (A_KSTR + A_VSTR) * sizeof(float);
+    return GLDS ? (size_t)2 * KTS * (2 * CH) * sizeof(float) : (size_t)2 * KTS * (A_KSTR + A_VSTR) * sizeof(float);
 }
 
 PDSC_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void *base, uint32_t bytes) {
@@ -75,7 +75,12 @@ PDSC_DEV void attention_block_coords(const AttnGrid &g, bool xcd, int &b, int &q
     b = r / g.nqb;
 }
 
-template <int NW, int KTS, bool FASTEXP, bool XCD, int BUF = 3>
+// GLDS: stage K/V with LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece = two
+// 512-B rows per wave-instruction, no staging registers).  K rows are stored
+// unpadded with their 16-B chunks XOR-swizzled by (row & 15) -- the swizzle is
+// applied to the SOURCE address (the DMA writes LDS lane-linearly) and undone on
+// the ds_read_b128 side, keeping the column reads conflict-free.
+template <int NW, int KTS, bool FASTEXP, bool XCD, int BUF = 3, bool GLDS = false>
 __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t(
     const float *__restrict__ q, const float *__restrict__ k, const float *__restrict__ v,
     const float *__restrict__ M, AttnGrid g, float *__restrict__ opart, float *__restrict__ ml) {
@@ -84,8 +89,9 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
     static_assert(LD4 * NT * 4 == KTS * CH, "stage must split evenly");
     constexpr float DEFER = FASTEXP ? 8.0f : 5.5f;    // log2 / ln units
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float *Kl0 = smem, *Kl1 = smem + KTS * A_KSTR;
-    float *Vl0 = smem + 2 * KTS * A_KSTR, *Vl1 = Vl0 + KTS * A_VSTR;
+    constexpr int KSTR_ = GLDS ? CH : A_KSTR;
+    float *Kl0 = smem, *Kl1 = smem + KTS * KSTR_;
+    float *Vl0 = smem + 2 * KTS * KSTR_, *Vl1 = Vl0 + KTS * A_VSTR;
 
     int b, qb, split;
     attention_block_coords(g, XCD, b, qb, split);
@@ -120,7 +126,22 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
         for (int i = 0; i < 64; ++i) qf[i] = 0.0f;
     }
 
-    f32x4 sk[LD4], sv[LD4];
+    f32x4 sk[GLDS ? 1 : LD4], sv[GLDS ? 1 : LD4];
+    // LDS-DMA staging: the stage is KTS*CH*4*2 bytes = 2*KTS/2 pieces of 1 KiB
+    constexpr int PIECES = KTS;  // KTS/2 K pieces + KTS/2 V pieces
+    auto glds_stage = [&](int st, float *Kl, float *Vl) {
+#pragma unroll
+        for (int i = 0; i < PIECES / NW; ++i) {
+            const int piece = wave * (PIECES / NW) + i;
+            const bool isV = piece >= PIECES / 2;
+            const int pp = isV ? piece - PIECES / 2 : piece;
+            const int row = 2 * pp + (lane >> 5), cpos = lane & 31;
+            const int csrc = isV ? cpos : (cpos ^ (row & 15));
+            const float *g = (isV ? v : k) + pbase + (size_t)(st * KTS + row) * CH + 4 * csrc;
+            float *l = (isV ? Vl : Kl) + pp * 256;
+            __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+        }
+    };
     auto load_stage = [&](int st) {
 #pragma unroll
         for (int i = 0; i < LD4; ++i) {
@@ -165,10 +186,10 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
             }
         }
         f32x16 S = zero16();
-        const float *Kp = Kl + l32 * A_KSTR + h * 64;
+        const float *Kp = Kl + l32 * KSTR_ + h * 64;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const f32x4 kv = *reinterpret_cast<const f32x4 *>(Kp + 4 * i);
+            const f32x4 kv = *reinterpret_cast<const f32x4 *>(Kp + 4 * (GLDS ? (i ^ (l32 & 15)) : i));
             S = mfma32(kv[0], qf[4 * i], S);
             S = mfma32(kv[1], qf[4 * i + 1], S);
             S = mfma32(kv[2], qf[4 * i + 2], S);
@@ -218,23 +239,32 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
     };
 
     if (st0 < st1) {
-        load_stage(st0);
-        store_stage(Kl0, Vl0);
+        if (GLDS) {
+            glds_stage(st0, Kl0, Vl0);
+        } else {
+            load_stage(st0);
+            store_stage(Kl0, Vl0);
+        }
     }
     __syncthreads();
     for (int st = st0; st < st1; ++st) {
         const int buf = (st - st0) & 1;
         const float *Kl = buf ? Kl1 : Kl0;
         const float *Vl = buf ? Vl1 : Vl0;
-        if (st + 1 < st1) load_stage(st + 1);
+        if (st + 1 < st1) {
+            if (GLDS)
+                glds_stage(st + 1, buf ? Kl0 : Kl1, buf ? Vl0 : Vl1);
+            else
+                load_stage(st + 1);
+        }
         if (active) {
 #pragma unroll
             for (int sub = 0; sub < KTS / 32; ++sub) {
                 const int key0 = st * KTS + sub * 32;
-                if (key0 < N) subtile(Kl + sub * 32 * A_KSTR, Vl + sub * 32 * A_VSTR, key0);
+                if (key0 < N) subtile(Kl + sub * 32 * KSTR_, Vl + sub * 32 * A_VSTR, key0);
             }
         }
-        if (st + 1 < st1) store_stage(buf ? Kl0 : Kl1, buf ? Vl0 : Vl1);
+        if (!GLDS && st + 1 < st1) store_stage(buf ? Kl0 : Kl1, buf ? Vl0 : Vl1);
         __syncthreads();
     }
     if (!active) return;

@@ -160,6 +160,9 @@ PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk,
     f32x4 wbuf[IN / 8];  // the wave's whole weight panel, issued up front
 #pragma unroll
     for (int g = 0; g < IN / 8; ++g) wbuf[g] = wp[g * 64];
+    // keep the scheduler from sinking the loads next to their uses (each would
+    // then expose a full L2 round trip every 8 MFMAs); waits stay counted
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int g = 0; g < IN / 8; ++g) {
         const f32x4 wb = wbuf[g];
@@ -235,7 +238,7 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
-__global__ __launch_bounds__(256) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
+__global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
                                                        size_t l0b, PwDense4 d,
                                                        const float *__restrict__ corr, int in_dim,
                                                        int N, int Npad, float *__restrict__ feat,
@@ -296,7 +299,7 @@ PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restric
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
+__global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
                                                      int Npad, float *__restrict__ feat,
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(256) void pw_mid_kernel(const float *__restrict__ p
     pcn_qkv(XB, XA, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
 }
 
-__global__ __launch_bounds__(256) void pw_last_kernel(
+__global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
     const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
     const float *__restrict__ feat, float *__restrict__ feat_out, float *__restrict__ normed,

@@ -1,0 +1,159 @@
+"""Registration evaluation harness, sharded over GPUs.
+
+Per-pair statistics rows with the columns of evaluation/test_3DMatch.py:90-101
+(and test_KITTI.py:118-129, whose column 11 is the ICP time instead of the
+scene index):
+
+  0 success  1 RE (deg)  2 TE (cm)  3 input inlier #  4 input inlier ratio
+  5 output inlier #  6 precision  7 recall  8 f1  9 model time  10 data time
+  11 scene index
+
+RE/TE/success follow libs/loss.py:12-59 (TransformationLoss; thresholds
+re_thre/te_thre from config.py:111-129: 15 deg / 30 cm for 3DMatch, 5 deg /
+60 cm for KITTI); precision/recall/f1 follow libs/loss.py:62-111
+(ClassificationLoss on pred_labels > 0, sklearn's zero_division=0 result).
+All statistics of a batch are computed at once on the device the poses live
+on; they are O(N) per pair and not on the hot path.
+
+Aggregation follows test_3DMatch.py:138-176: per-scene means (RE/TE over the
+successful pairs only), the mean over scenes, and the all-pair means.  Across
+ranks the rows are all-gathered (pointdsc_amd.dist.gather_rows) so the
+all-pair means are exact; the reference's KITTI driver instead all-reduces
+per-rank averages (test_KITTI.py:169-185), which weighs ranks equally.
+"""
+import math
+
+import numpy as np
+import torch
+
+COLUMNS = ["success", "re_deg", "te_cm", "input_inliers", "input_inlier_ratio", "output_inliers",
+           "precision", "recall", "f1", "model_time", "data_time", "scene"]
+THRESHOLDS = {"3dmatch": (15.0, 30.0), "kitti": (5.0, 60.0)}  # (re_thre deg, te_thre cm)
+
+
+def pair_stats(trans, gt_trans, pred_labels, gt_labels, re_thre=15.0, te_thre=30.0):
+    """[B, 9] float64 rows (columns 0-8) for a batch of B pairs.
+
+    trans, gt_trans [B,4,4]; pred_labels, gt_labels [B,N] (0/1)."""
+    trans, gt_trans = trans.float(), gt_trans.float()
+    R, t = trans[:, :3, :3], trans[:, :3, 3]
+    gR, gt_t = gt_trans[:, :3, :3], gt_trans[:, :3, 3]
+    # libs/loss.py:44-49: acos(clamp((tr(R^T R_gt) - 1)/2)) in deg, |t - t_gt| in cm
+    tr = torch.diagonal(R.transpose(1, 2) @ gR, dim1=1, dim2=2).sum(-1)
+    re = torch.acos(torch.clamp((tr - 1) / 2.0, min=-1, max=1)) * 180 / np.pi
+    te = torch.sqrt(torch.sum((t - gt_t) ** 2, dim=-1)) * 100
+    success = ((te < te_thre) & (re < re_thre)).double()
+    gt = gt_labels > 0
+    pred = pred_labels > 0
+    n_in = gt.sum(-1).double()
+    tp = (gt & pred).sum(-1).double()
+    n_pred = pred.sum(-1).double()
+    precision = torch.where(n_pred > 0, tp / n_pred.clamp(min=1), torch.zeros_like(tp))
+    recall = torch.where(n_in > 0, tp / n_in.clamp(min=1), torch.zeros_like(tp))
+    denom = precision + recall
+    f1 = torch.where(denom > 0, 2 * precision * recall / denom.clamp(min=1e-300), torch.zeros_like(tp))
+    ratio = gt_labels.float().mean(-1).double()
+    return torch.stack([success, re.double(), te.double(), n_in, ratio, tp, precision, recall, f1], dim=1)
+
+
+def _mean_success_only(stats, col):
+    ok = stats[:, 0] == 1
+    return float(stats[ok, col].mean()) if ok.any() else math.nan
+
+
+def aggregate(stats, n_scenes=None):
+    """Scene-level and all-pair summaries of [P, 12] rows (numpy float64),
+    as test_3DMatch.py:141-176 logs them."""
+    stats = np.asarray(stats, dtype=np.float64)
+    out = {"pairs": int(stats.shape[0])}
+    scenes = sorted(set(stats[:, 11].astype(int).tolist())) if n_scenes is None else list(range(n_scenes))
+    vals = []
+    for s in scenes:
+        st = stats[stats[:, 11].astype(int) == s]
+        if len(st) == 0:
+            continue
+        v = st.mean(0)
+        v[1], v[2] = _mean_success_only(st, 1), _mean_success_only(st, 2)
+        vals.append(v)
+    if vals:
+        avg = np.stack(vals).mean(0)
+        out["scene_mean"] = {c: float(avg[i]) for i, c in enumerate(COLUMNS[:11])}
+    allp = stats.mean(0)
+    out["all_pairs"] = {c: float(allp[i]) for i, c in enumerate(COLUMNS[:11])}
+    out["all_pairs"]["re_deg"] = _mean_success_only(stats, 1)
+    out["all_pairs"]["te_cm"] = _mean_success_only(stats, 2)
+    return out
+
+
+def evaluate_synthetic(model, n_pairs, num_corr, preset="3dmatch", batch=16, seed=0, device=None,
+                       inlier_ratio=0.3):
+    """Sharded evaluation over n_pairs synthetic pairs: rank r evaluates pairs
+    r, r+W, ... in batches through the batched forward, then the [n_pairs, 12]
+    stats matrix is all-gathered.  Returns (stats numpy, summary dict)."""
+    import time
+    from . import dist
+    from .synthetic import synthetic_pair
+    rank, W = dist.world()
+    mine = dist.shard_indices(n_pairs, rank, W)
+    re_thre, te_thre = THRESHOLDS[preset]
+    rows = []
+    for b0 in range(0, len(mine), batch):
+        idx = mine[b0:b0 + batch]
+        t0 = time.perf_counter()
+        ps = [synthetic_pair(num_corr, seed * 100003 + i, preset=preset, inlier_ratio=inlier_ratio) for i in idx]
+        corr, src, tgt, gtT, gtL = (torch.from_numpy(np.stack([p[k] for p in ps])).to(device)
+                                    for k in ("corr_pos", "src_keypts", "tgt_keypts", "gt_trans", "gt_labels"))
+        if device is not None and device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t_data = (time.perf_counter() - t0) / len(idx)
+        t0 = time.perf_counter()
+        T, L = model.forward_batched(corr, src, tgt)
+        if device is not None and device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t_model = (time.perf_counter() - t0) / len(idx)
+        st = pair_stats(T, gtT, L, gtL, re_thre, te_thre).cpu()
+        extra = torch.tensor([[t_model, t_data, 0.0]], dtype=torch.float64).expand(len(idx), 3)
+        rows.append(torch.cat([st, extra], dim=1))
+    mine_rows = torch.cat(rows) if rows else torch.zeros((0, 12), dtype=torch.float64)
+    gdev = device if (W > 1 and device is not None and device.type == "cuda") else None
+    allrows = dist.gather_rows(mine_rows, n_pairs, device=gdev).cpu().numpy()
+    return allrows, aggregate(allrows)
+
+
+def main():
+    """torchrun entry: python -m torch.distributed.run --nproc-per-node W
+    -m pointdsc_amd.evaluate --pairs 256 --num-corr 1000"""
+    import argparse
+    import json
+    import os
+    import torch.distributed as tdist
+    from .PointDSC import PointDSC
+    from .synthetic import PRESETS, trained_state_dict
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=64)
+    ap.add_argument("--num-corr", type=int, default=1000)
+    ap.add_argument("--preset", default="3dmatch", choices=list(PRESETS))
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--inlier-ratio", type=float, default=0.3)
+    a = ap.parse_args()
+    W = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if W > 1:
+        tdist.init_process_group("nccl", init_method="env://")
+    p = PRESETS[a.preset]
+    m = PointDSC(num_layers=12, inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"],
+                 nms_radius=p["nms_radius"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict(a.preset).items()})
+    m = m.to(dev).eval()
+    stats, summary = evaluate_synthetic(m, a.pairs, a.num_corr, a.preset, a.batch, device=dev,
+                                        inlier_ratio=a.inlier_ratio)
+    if not tdist.is_initialized() or tdist.get_rank() == 0:
+        print(json.dumps(summary))
+    if W > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -149,6 +149,51 @@ def test_batched_equals_single(gpu_device):
         np.testing.assert_allclose(r["final_trans"][0].cpu().numpy(), T[i].cpu().numpy(), atol=1e-5)
 
 
+def test_graph_replay_equals_eager(gpu_device):
+    """ForwardPlan.capture(): a HIP-graph replay of the forward gives the eager
+    result bitwise, and picks up new contents of the same input buffers; the
+    stage-timing hook records 8 events per forward."""
+    import ctypes
+    from pointdsc_amd import _lib, kernels
+    from pointdsc_amd.synthetic import synthetic_batch
+    g = load_golden("rel_1k")
+    m = _model(g, gpu_device)
+    cfg, packed = m.pdsc_config(), m.packed_weights()
+    b1, b2 = synthetic_batch(2, 1000, seed=11), synthetic_batch(2, 1000, seed=12)
+    corr, src, tgt = (_t(b1[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    eager = kernels.ForwardPlan(cfg, packed, 2, 1000, gpu_device)
+    T1, L1 = (x.clone() for x in eager.run(corr, src, tgt))
+    graph = kernels.ForwardPlan(cfg, packed, 2, 1000, gpu_device).capture(corr, src, tgt)
+    Tg, Lg = graph.run(corr, src, tgt)
+    assert torch.equal(T1, Tg) and torch.equal(L1, Lg)
+    for x, k in zip((corr, src, tgt), ("corr_pos", "src_keypts", "tgt_keypts")):
+        x.copy_(_t(b2[k], gpu_device))
+    T2, L2 = (x.clone() for x in eager.run(corr, src, tgt))
+    Tg, Lg = graph.run(corr, src, tgt)
+    assert torch.equal(T2, Tg) and torch.equal(L2, Lg) and not torch.equal(T1, T2)
+    # stage timing hook
+    hip = ctypes.CDLL("libamdhip64.so")
+    ev = (ctypes.c_void_p * 16)()
+    for i in range(16):
+        e = ctypes.c_void_p()
+        assert hip.hipEventCreate(ctypes.byref(e)) == 0
+        ev[i] = e.value
+    cnt = ctypes.c_int32(0)
+    L = _lib.load()
+    _lib.check(L.pdsc_forward_timing(ev, 16, ctypes.byref(cnt)), "pdsc_forward_timing")
+    for _ in range(3):
+        eager.run(corr, src, tgt)
+    L.pdsc_forward_timing(None, 0, None)
+    torch.cuda.synchronize(gpu_device)
+    assert cnt.value == 16  # the third call did not fit
+    ms = ctypes.c_float()
+    for i in range(7):
+        assert hip.hipEventElapsedTime(ctypes.byref(ms), ctypes.c_void_p(ev[i]), ctypes.c_void_p(ev[i + 1])) == 0
+        assert ms.value >= 0
+    for i in range(16):
+        hip.hipEventDestroy(ctypes.c_void_p(ev[i]))
+
+
 def test_attention_vs_torch_fp32(gpu_device):
     """The attention kernel against a plain PyTorch fp32 reference of :36-42."""
     from pointdsc_amd import kernels

@@ -34,13 +34,13 @@ struct Variant {
     void (*launch)(const float *, const float *, const float *, const float *, int, int, float *, float *, float *, hipStream_t);
 };
 
-template <int NW, int KTS, bool FE, bool XCD, int BUF = 3>
+template <int NW, int KTS, bool FE, bool XCD, int BUF = 3, bool GL = false>
 void run_variant(const float *q, const float *k, const float *v, const float *M, int B, int N, float *op,
                  float *ml, float *out, hipStream_t s) {
     AttnGrid g = attention_grid<NW, KTS>(B, N, 1024);
     const int G = g.B * g.nqb * g.nsplit;
-    const size_t lds = attention_lds_bytes<NW, KTS>();
-    auto kern = attention_kernel_t<NW, KTS, FE, XCD, BUF>;
+    const size_t lds = attention_lds_bytes<NW, KTS, GL>();
+    auto kern = attention_kernel_t<NW, KTS, FE, XCD, BUF, GL>;
     hipLaunchKernelGGL(kern, dim3(G), dim3(NW * 64), lds, s, q, k, v, M, g, op, ml);
     CK(hipGetLastError());
     if (out) hipLaunchKernelGGL(combine_k, dim3(N, B), dim3(CH), 0, s, op, ml, N, g.Npad, g.nsplit, out);
@@ -51,21 +51,10 @@ int main(int argc, char **argv) {
     int iters = argc > 3 ? atoi(argv[3]) : 20;
     const int Npad = round_up(N, QB);
     std::vector<Variant> V = {
-        {"nw4 kt32 expf   xcd0", run_variant<4, 32, false, false>},
-        {"nw4 kt32 exp2   xcd0", run_variant<4, 32, true, false>},
-        {"nw4 kt32 expf nobuf  ", run_variant<4, 32, false, false, 0>},
-        {"nw4 kt32 expf bufKV  ", run_variant<4, 32, false, false, 1>},
-        {"nw4 kt32 expf bufM   ", run_variant<4, 32, false, false, 2>},
-        {"nw4 kt32 exp2   xcd1", run_variant<4, 32, true, true>},
-        {"nw8 kt64 exp2   xcd1", run_variant<8, 64, true, true>},
-        {"nw8 kt32 exp2   xcd1", run_variant<8, 32, true, true>},
-        {"nw8 kt64 expf   xcd1", run_variant<8, 64, false, true>},
+        {"nw4 kt32 exp2 xcd1     ", run_variant<4, 32, true, true>},
+        {"nw4 kt32 exp2 xcd1 glds", run_variant<4, 32, true, true, 3, true>},
+        {"nw4 kt32 expf xcd1 glds", run_variant<4, 32, false, true, 3, true>},
     };
-    const int lds64 = (int)attention_lds_bytes<8, 64>();
-    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&attention_kernel_t<8, 64, true, true>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, lds64));
-    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(&attention_kernel_t<8, 64, false, true>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, lds64));
     size_t nq = (size_t)B * Npad * CH;
     std::vector<float> hq(nq * 3, 0.f), hp((size_t)B * N * 6);
     srand(1);

@@ -29,11 +29,11 @@ def main(tag, src=None):
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     pmc = defaultdict(lambda: defaultdict(list))
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        p = os.path.join(src, f"pmc_{ctr}", "run_counter_collection.csv")
-        if os.path.exists(p):
-            for r in csv.DictReader(open(p)):
-                pmc[short(r["Kernel_Name"])][ctr].append(float(r["Counter_Value"]))
+    import glob
+    for p in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(p)):
+            pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    extra = sorted({c for k in pmc.values() for c in k} - {"FETCH_SIZE", "WRITE_SIZE"})
     lines = [f"# rocprofv3 summary `{tag}`", "",
              "Kernel-trace stats (`rocprofv3 --kernel-trace --stats`) and per-dispatch HBM counters "
              "from separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes of the same command "
@@ -49,6 +49,13 @@ def main(tag, src=None):
         lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
                      f"{float(r['TotalDurationNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} | "
                      f"{fa:.0f} | {2 * fa * 1024 / 1e6:.1f} | {wa:.0f} |")
+    if extra:
+        lines += ["", "Other counters (mean per dispatch):", "",
+                  "| kernel | " + " | ".join(extra) + " |", "|---|" + "---|" * len(extra)]
+        for r in rows:
+            k = short(r["Name"])
+            vals = [sum(pmc[k][c]) / len(pmc[k][c]) if pmc[k][c] else float("nan") for c in extra]
+            lines.append(f"| {k} | " + " | ".join(f"{v:.4g}" for v in vals) + " |")
     out = os.path.join(dst, f"{tag}_summary.md")
     open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
