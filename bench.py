@@ -33,6 +33,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, v_mfma_f32_32x32x2_f32
+PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense v_mfma_f32_32x32x16_f16
+# the attention computes each fp32 product as 3 fp16 MFMA products (hi.hi + hi.lo + lo.hi,
+# attention_h3.hpp): its ceiling in ALGORITHMIC (fp32) flop/s is the fp16 peak / 3
+PEAK_H3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E spec
 
 
@@ -221,9 +225,12 @@ def main():
         att_ms = sum(att_times) / len(att_times)
         flops = P * 4.0 * N * N * 128
         achieved = flops / (att_ms * 1e-3) / 1e12
-        roofline = {"kernel": "attention_kernel_t<4,32,exp2,xcd>", "bound": "mfma",
-                    "achieved": round(achieved, 3), "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None,
+        roofline = {"kernel": "attention_h3_kernel<4,xcd>", "bound": "mfma",
+                    "achieved": round(achieved, 3), "peak": round(PEAK_H3_TFLOPS, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_H3_TFLOPS, 4), "traffic": None,
+                    "peak_note": "fp16 MFMA 2500 TFLOP/s / 3 products per fp32 product; "
+                                 "exact-fp32 MFMA peak is 157.3",
+                    "fp16_mfma_util": round(3 * achieved / PEAK_F16_MFMA_TFLOPS, 4),
                     "launch_ms": round(att_ms, 4), "launches_timed": len(att_times),
                     "flop_per_launch": flops, "share_of_step": round(12 * att_ms / ms_per_step, 3)}
         sp = ctypes.c_void_p(stream.cuda_stream)

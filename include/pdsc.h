@@ -98,10 +98,9 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
                            int32_t B, int32_t N, int32_t C, float *msg, void *workspace,
                            size_t workspace_bytes, pdsc_stream_t stream);
 
-/* The attention kernel exactly as the encoder launches it, for measurement:
- * q/k/v are PADDED [B,Npad,C] (rows >= N zero, Npad and nsplit from
- * pdsc_attention_layout); outputs the split partials opart [B,nsplit,Npad,C]
- * (unnormalised) and ml [B,nsplit,Npad,2] (running max, sum).               */
+/* The encoder's attention geometry for (B, N): padded rows per pair and the
+ * number of key splits (partials opart [B,nsplit,Npad,C], ml [B,nsplit,Npad,2]
+ * live in the encoder workspace).                                           */
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit);
 
 /* Measurement hook (bench.py): while capacity > 0, every attention launch the
@@ -118,9 +117,6 @@ int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_event
  * *count += 8, while *count + 8 <= capacity.  Capacity 0 disables.           */
 #define PDSC_FORWARD_STAGES 7
 int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *count);
-int32_t pdsc_attention_partials_f32(const float *q_pad, const float *k_pad, const float *v_pad,
-                                    const float *M, int32_t B, int32_t N, float *opart, float *ml,
-                                    pdsc_stream_t stream);
 
 /* ------------------------------------------------------- a5 seeds ----------
  * pick_seeds: radius NMS on the confidences then the top-S of

@@ -50,7 +50,6 @@ _PROTOS = {
     "pdsc_attention_layout": (c_int32, [c_int32, c_int32, ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)]),
     "pdsc_attention_timing": (c_int32, [ctypes.POINTER(vp), ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_forward_timing": (c_int32, [ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
-    "pdsc_attention_partials_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp]),
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
     "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),

@@ -88,16 +88,17 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
 }
 
 struct EncBufs {
-    float *feat, *q, *k, *v, *opart, *ml;
+    float *feat, *opart, *ml;
+    _Float16 *q, *k, *v;  // attention_h3 split layouts (hi + lo per element)
 };
 
 EncBufs carve_encoder(Carve &c, const Dims &d) {
     EncBufs e;
     const size_t rows = (size_t)d.B * d.Npad * CH;
     e.feat = c.take<float>(rows);
-    e.q = c.take<float>(rows);
-    e.k = c.take<float>(rows);
-    e.v = c.take<float>(rows);
+    e.q = c.take<_Float16>(2 * rows);
+    e.k = c.take<_Float16>(2 * rows);
+    e.v = c.take<_Float16>(2 * rows);
     e.opart = c.take<float>(rows * d.nsplit);
     e.ml = c.take<float>((size_t)d.B * d.Npad * d.nsplit * 2);
     return e;
@@ -304,7 +305,7 @@ size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
     if (C != CH || B < 1 || N < 1) return 0;
     const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
     Carve c(nullptr);
-    for (int i = 0; i < 3; ++i) c.take<float>((size_t)B * Npad * CH);
+    for (int i = 0; i < 3; ++i) c.take<_Float16>((size_t)2 * B * Npad * CH);
     c.take<float>((size_t)B * Npad * CH * ns);
     c.take<float>((size_t)B * Npad * ns * 2);
     return c.off;
@@ -320,19 +321,14 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     hipStream_t s = S_(stream);
     const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
     Carve c(ws);
-    float *qp = c.take<float>((size_t)B * Npad * CH);
-    float *kp = c.take<float>((size_t)B * Npad * CH);
-    float *vp = c.take<float>((size_t)B * Npad * CH);
+    _Float16 *qs = c.take<_Float16>((size_t)2 * B * Npad * CH);
+    _Float16 *ks = c.take<_Float16>((size_t)2 * B * Npad * CH);
+    _Float16 *vs = c.take<_Float16>((size_t)2 * B * Npad * CH);
     float *op = c.take<float>((size_t)B * Npad * CH * ns);
     float *ml = c.take<float>((size_t)B * Npad * ns * 2);
-    // re-pad the caller's [B][N][C] rows to the kernel's [B][Npad][C] (zero rows)
-    const size_t pad_bytes = (size_t)B * Npad * CH * sizeof(float);
-    for (float *p : {qp, kp, vp}) HIPCHK(hipMemsetAsync(p, 0, pad_bytes, s));
-    const size_t row = CH * sizeof(float);
-    HIPCHK(hipMemcpy2DAsync(qp, Npad * row, q, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpy2DAsync(kp, Npad * row, k, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpy2DAsync(vp, Npad * row, v, N * row, N * row, B, hipMemcpyDeviceToDevice, s));
-    HIPCHK(launch_attention(qp, kp, vp, M, B, N, Npad, ns, op, ml, s));
+    // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
+    HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, s));
+    HIPCHK(launch_attention(qs, ks, vs, M, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
@@ -360,15 +356,6 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nspl
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
     *nsplit = attention_nsplit(B, N);
-    return PDSC_OK;
-}
-
-int32_t pdsc_attention_partials_f32(const float *q, const float *k, const float *v, const float *M,
-                                    int32_t B, int32_t N, float *opart, float *ml, pdsc_stream_t stream) {
-    if (!q || !k || !v || !M || !opart || !ml) return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || N < 1 || N > 32767) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
-    HIPCHK(launch_attention(q, k, v, M, B, N, round_up(N, QB), attention_nsplit(B, N), opart, ml,
-                            S_(stream)));
     return PDSC_OK;
 }
 

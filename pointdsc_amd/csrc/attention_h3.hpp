@@ -1,0 +1,294 @@
+// attention_h3.hpp -- the SCNonlocal attention core (models/PointDSC.py:36-42)
+// on the fp16 matrix cores with fp32-equivalent accuracy ("3xf16").
+//
+//   msg_i = sum_j softmax_j( M_ij * (q_i . k_j) / sqrt(C) ) v_j,   C = 128, heads = 1
+//
+// gfx950 has no reduced-precision fp32 MFMA (v_mfma_f32_32x32x2_f32 runs at
+// the fp32 vector rate, 1/16 of v_mfma_f32_32x32x16_f16).  Every fp32 operand
+// x is stored as an exact-sum pair x = hi + lo of fp16 values (hi = fp16(x),
+// lo = fp16(x - hi): 22 significant bits) and each product is formed from the
+// three significant partial products
+//      a.b ~= a_hi.b_hi + a_hi.b_lo + a_lo.b_hi        (the a_lo.b_lo term is 2^-22 relative)
+// accumulated in fp32 by the MFMA -- 3 fp16 MFMAs instead of 16 fp32 ones.
+// Validated against the reference's golden features (tools/emulate_h3.py):
+// the error vs the reference is the same as a plain fp32 re-ordering.
+//
+// Range: |Q|, |K|, |V| < 65504 (fp16 max; the features of the BN-normalised
+// encoder are O(10)); a value outside turns the result into inf/NaN (loud,
+// never silently wrong).  Softmax weights are kept as p = 2^(x - m + PSHIFT)
+// <= 2^(DEFER + PSHIFT) = 2^15, so they too sit in fp16's normal range.
+//
+// HBM layouts (written by the pointwise kernels' epilogues, encoder.hip, or
+// by split_qkv_kernel for the standalone API), per pair, Npad rows:
+//   Qs [Npad][2][128] fp16   row = query; [0] = hi, [1] = lo; channels in
+//                            qk_pos order (bits 2 and 3 of the index swapped)
+//   Ks [Npad][2][128] fp16   as Qs, and each 16-B chunk c of a row stored at
+//                            chunk c ^ (row & 15) (conflict-free LDS reads)
+//   Vs [Npad/32][2][128][32] per 32-key tile: hi plane, lo plane; plane row
+//                            rho(c) = 32 (c & 3) + (c >> 2); keys in v_keypos
+//                            order; 16-B chunk c of a row at c ^ ((rho >> 2) & 3)
+// Each layout equals the fp32 tensor's size (4 B per element).
+//
+// Work decomposition (as attention.hpp): a workgroup = NW waves x 32 queries
+// of one pair and a contiguous split of 32-key tiles; K and V tiles (16 KiB
+// each, contiguous in HBM) are copied into a 2-deep LDS ring by LDS-DMA.  Per
+// wave and tile:
+//   S^T = K Q^T      8 k-steps x 3 MFMA 32x32x16 (lane <-> query)
+//   logits, online softmax with a lazily re-based max (as attention.hpp)
+//   O  += P V        the S^T accumulator registers 8s..8s+7 ARE the A operand
+//                    of k-step s (key order = v_keypos), 4 channel tiles x 2 x 3 MFMA
+#pragma once
+#include "pdsc_internal.hpp"
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+namespace pdsc {
+
+constexpr int H3_ROWB = 2 * CH * 2;          // bytes per Qs/Ks row (hi + lo)
+constexpr int H3_TILE = 32;                  // keys per LDS tile
+constexpr int H3_KTB = H3_TILE * H3_ROWB;    // K tile bytes (16 KiB)
+constexpr int H3_VTB = 2 * CH * H3_TILE * 2; // V tile bytes (16 KiB)
+constexpr int H3_PSHIFT = 7;                 // p = 2^(x - m + PSHIFT)
+constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by > 2^8
+
+// channel -> position in a Qs/Ks row: swap bits 2 and 3
+PDSC_DEV constexpr int qk_pos(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
+// key (0..31 within a tile) -> position in a Vs plane row: swap bits 2 and 3
+PDSC_DEV constexpr int v_keypos(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
+// channel -> row of a Vs plane
+PDSC_DEV constexpr int v_rho(int c) { return 32 * (c & 3) + (c >> 2); }
+
+// element offsets (in fp16 units) inside one pair's buffers
+PDSC_DEV size_t qs_off(int row, int half, int c) { return (size_t)row * 2 * CH + half * CH + qk_pos(c); }
+PDSC_DEV size_t ks_off(int row, int half, int c) {
+    const int p = qk_pos(c);
+    return (size_t)row * 2 * CH + half * CH + 8 * ((p >> 3) ^ (row & 15)) + (p & 7);
+}
+PDSC_DEV size_t vs_off(int key, int half, int c) {
+    const int rho = v_rho(c), kp = v_keypos(key & 31);
+    return (size_t)(key >> 5) * (2 * CH * H3_TILE) + (size_t)half * CH * H3_TILE + rho * H3_TILE +
+           8 * ((kp >> 3) ^ ((rho >> 2) & 3)) + (kp & 7);
+}
+
+PDSC_DEV void split_h(float x, _Float16 &hi, _Float16 &lo) {
+    hi = (_Float16)x;
+    lo = (_Float16)(x - (float)hi);
+}
+
+PDSC_DEV f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// a.b with a = ah + al, b = bh + bl: small terms first
+PDSC_DEV f32x16 mfma_h3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x16 c) {
+    c = mfma_h(al, bh, c);
+    c = mfma_h(ah, bl, c);
+    return mfma_h(ah, bh, c);
+}
+
+template <int NW>
+constexpr size_t attention_h3_lds_bytes() { return (size_t)2 * (H3_KTB + H3_VTB); }
+
+PDSC_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+}
+
+struct AttnGridH3 {
+    int B, N, Npad, nqb, nsplit, sps;  // sps = 32-key tiles per split
+};
+
+template <int NW>
+inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
+    AttnGridH3 g;
+    g.B = B;
+    g.N = N;
+    g.Npad = round_up(N, QB);
+    g.nqb = (N + NW * 32 - 1) / (NW * 32);
+    const int nst = (N + H3_TILE - 1) / H3_TILE;
+    int ns = (target + B * g.nqb - 1) / (B * g.nqb);
+    ns = std::max(1, std::min(ns, std::max(1, nst / 2)));
+    g.sps = (nst + ns - 1) / ns;
+    g.nsplit = (nst + g.sps - 1) / g.sps;
+    return g;
+}
+
+template <int NW, bool XCD>
+__global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart, float *__restrict__ ml) {
+    extern __shared__ __attribute__((aligned(16))) char h3smem[];
+    // block -> (pair, query block, split), a pair's blocks kept on one XCD
+    const int G = g.B * g.nqb * g.nsplit;
+    int lid = blockIdx.x;
+    if (XCD) {
+        const int full = G & ~7;
+        if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
+    }
+    const int split = lid % g.nsplit;
+    const int qb = (lid / g.nsplit) % g.nqb;
+    const int b = lid / g.nsplit / g.nqb;
+
+    const int N = g.N, Npad = g.Npad;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int q0 = qb * (NW * 32) + wave * 32;
+    const int nst = (N + H3_TILE - 1) / H3_TILE;
+    const int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
+    const int qq = q0 + l32;
+    const bool active = q0 < Npad;
+
+    const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
+    const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
+    const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M + (size_t)b * N * N, (uint32_t)N * (uint32_t)N * 4u);
+
+    // this lane's query: 8 k-steps x (hi, lo) fragments, chunk 2j + h of its row
+    f16x8 qh[8], ql[8];
+    {
+        const char *qrow = reinterpret_cast<const char *>(Qs + ((size_t)b * Npad + min(qq, Npad - 1)) * 2 * CH);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            qh[j] = *reinterpret_cast<const f16x8 *>(qrow + 16 * (2 * j + h));
+            ql[j] = *reinterpret_cast<const f16x8 *>(qrow + CH * 2 + 16 * (2 * j + h));
+        }
+    }
+
+    // LDS-DMA copy of tile st (K 16 KiB + V 16 KiB = 32 pieces of 1 KiB) into ring slot `slot`
+    auto stage = [&](int st, int slot) {
+        char *dst = h3smem + slot * (H3_KTB + H3_VTB);
+        constexpr int PIECES = (H3_KTB + H3_VTB) / 1024;
+#pragma unroll
+        for (int i = 0; i < PIECES / NW; ++i) {
+            const int piece = wave * (PIECES / NW) + i;
+            const char *src = piece < H3_KTB / 1024
+                                  ? Kp + (size_t)st * H3_KTB + piece * 1024
+                                  : Vp + (size_t)st * H3_VTB + (piece - H3_KTB / 1024) * 1024;
+            __builtin_amdgcn_global_load_lds(src + 16 * lane, dst + piece * 1024, 16, 0, 0);
+        }
+    };
+
+    f32x16 O[4] = {zero16(), zero16(), zero16(), zero16()};
+    float m_run = -INFINITY, l_run = 0.0f;
+    const float scale = 0.12751743082459868f;  // log2(e) / sqrt(128)
+    const uint32_t Nb = (uint32_t)N * 4;
+
+    auto tile = [&](const char *Kl, const char *Vl, int key0) {
+        // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys, issued first
+        float mv[16];
+        const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            mv[r] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb, 0, 0));
+        // S^T[key][query] = sum_c K[key][c] Q[query][c]
+        f32x16 S = zero16();
+        const char *krow = Kl + l32 * H3_ROWB;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ch = (2 * j + h) ^ (l32 & 15);
+            const f16x8 kh = *reinterpret_cast<const f16x8 *>(krow + 16 * ch);
+            const f16x8 kl = *reinterpret_cast<const f16x8 *>(krow + CH * 2 + 16 * ch);
+            S = mfma_h3(kh, kl, qh[j], ql[j], S);
+        }
+        float p[16];
+        float mx = -INFINITY;
+        const bool tail = key0 + 32 > N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float x = mv[r] * (S[r] * scale);  // (:39) then * M (:41); 0, not -inf, off-support
+            if (tail && key0 + acc_row(r, h) >= N) x = -INFINITY;
+            p[r] = x;
+            mx = fmaxf(mx, x);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        if (__any(mx > m_run + H3_DEFER)) {  // wave-uniform re-base of the running max
+            const float m_new = fmaxf(m_run, mx);
+            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            m_run = m_new;
+            l_run *= alpha;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float a = __shfl(alpha, acc_row(r, h));
+#pragma unroll
+                for (int t = 0; t < 4; ++t) O[t][r] *= a;
+            }
+        }
+        const float mb = m_run - (float)H3_PSHIFT;
+        float psum = 0.0f;
+        f16x8 ph[2], pl[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = __builtin_amdgcn_exp2f(p[r] - mb);
+            psum += e;
+            _Float16 hi, lo;
+            split_h(e, hi, lo);
+            ph[r >> 3][r & 7] = hi;
+            pl[r >> 3][r & 7] = lo;
+        }
+        l_run += psum;
+        // O[query][4 l32 + t] += sum_key P[query][key] V[key][4 l32 + t]
+        const int sw = (l32 >> 2) & 3;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const char *vrow = Vl + (32 * t + l32) * (H3_TILE * 2);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int ch = (2 * s + h) ^ sw;
+                const f16x8 vh = *reinterpret_cast<const f16x8 *>(vrow + 16 * ch);
+                const f16x8 vl = *reinterpret_cast<const f16x8 *>(vrow + CH * H3_TILE * 2 + 16 * ch);
+                O[t] = mfma_h3(ph[s], pl[s], vh, vl, O[t]);
+            }
+        }
+    };
+
+    if (st0 < st1) stage(st0, 0);
+    __syncthreads();
+    for (int st = st0; st < st1; ++st) {
+        const int slot = (st - st0) & 1;
+        if (st + 1 < st1) stage(st + 1, slot ^ 1);
+        if (active) {
+            const char *base = h3smem + slot * (H3_KTB + H3_VTB);
+            tile(base, base + H3_KTB, st * H3_TILE);
+        }
+        __syncthreads();
+    }
+    if (!active) return;
+
+    l_run += __shfl_xor(l_run, 32);
+    const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
+    float *Ob = opart + obase * CH;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = q0 + acc_row(r, h);
+        *reinterpret_cast<f32x4 *>(Ob + (size_t)row * CH + 4 * l32) = f32x4{O[0][r], O[1][r], O[2][r], O[3][r]};
+    }
+    if (h == 0) {
+        // partial max in natural-log units (the p's carry the 2^PSHIFT factor)
+        ml[(obase + qq) * 2] = (m_run - (float)H3_PSHIFT) * 0.6931471805599453f;
+        ml[(obase + qq) * 2 + 1] = l_run;
+    }
+}
+
+// fp32 q, k, v [B][ld][CH] (ld >= N rows per pair; rows >= N of the padded
+// layouts become zero) -> Qs, Ks, Vs.  One thread per (pair, row, channel).
+__global__ void split_qkv_kernel(const float *__restrict__ q, const float *__restrict__ k,
+                                 const float *__restrict__ v, int B, int N, int ld, int Npad,
+                                 _Float16 *__restrict__ Qs, _Float16 *__restrict__ Ks,
+                                 _Float16 *__restrict__ Vs) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)B * Npad * CH) return;
+    const int c = (int)(i % CH);
+    const int row = (int)((i / CH) % Npad);
+    const int b = (int)(i / CH / Npad);
+    const size_t src = ((size_t)b * ld + row) * CH + c, pb = (size_t)b * Npad * 2 * CH;
+    const bool in = row < N;
+    _Float16 hi, lo;
+    split_h(in ? q[src] : 0.0f, hi, lo);
+    Qs[pb + qs_off(row, 0, c)] = hi;
+    Qs[pb + qs_off(row, 1, c)] = lo;
+    split_h(in ? k[src] : 0.0f, hi, lo);
+    Ks[pb + ks_off(row, 0, c)] = hi;
+    Ks[pb + ks_off(row, 1, c)] = lo;
+    split_h(in ? v[src] : 0.0f, hi, lo);
+    Vs[pb + vs_off(row, 0, c)] = hi;
+    Vs[pb + vs_off(row, 1, c)] = lo;
+}
+
+}  // namespace pdsc

@@ -2,25 +2,26 @@
 //
 // Replaces models/PointDSC.py:9-77 (NonLocalBlock / NonLocalNet), :155-156 and
 // :171.  Layout in HBM (per pair b, N padded to Npad = round_up(N,128) rows):
-//   feat, Q, K, V : [B][Npad][128] fp32, point-major (row = correspondence)
+//   feat          : [B][Npad][128] fp32, point-major (row = correspondence)
+//   Qs, Ks, Vs    : the fp16 hi/lo split layouts of attention_h3.hpp (4 B/element)
 //   M             : [B][N][N] fp32 (a1 output; symmetric)
 //   opart, ml     : [B][nsplit][Npad][128], [B][nsplit][Npad][2] attention partials
 //
 // Kernels per forward: pw_first (layer0 + PointCN_0 + QKV_0), then per layer
 // attention_l (+ pw_mid_l = combine + fc_message_l + residual + PointCN_{l+1}
 // + QKV_{l+1}), and pw_last (combine + fc_message + residual + normalize +
-// classifier).  All products run on v_mfma_f32_32x32x2_f32 (exact fp32 fma
-// chains; gfx950 has no reduced-precision fp32 MFMA), so the encoder is bound
-// by the 157 TFLOP/s fp32 matrix roofline: 4 N^2 C flop per layer of attention.
+// classifier).  The pointwise products run on v_mfma_f32_32x32x2_f32 (exact
+// fp32 fma chains); their Q/K/V epilogues write the fp16 hi/lo splits that the
+// attention consumes.
 //
-// Attention (flash-style, never materialising the N x N logits):
-//   one workgroup = 4 waves x 32 queries; K/V tiles of 32 keys double-buffered
-//   in LDS; S^T = K Q^T so the accumulator's column index is the query and it
-//   feeds P.V as the A operand with no transpose; logits = M_ij * s_ij / sqrt(C)
-//   where M is read column-wise (M symmetric => coalesced 128-B rows);
-//   incompatible pairs keep logit 0 (not -inf) exactly as :41; online softmax
-//   with a running max; split-K over keys when B*N is too small to fill 256 CUs.
-#include "attention.hpp"
+// Attention (attention_h3.hpp; flash-style, never materialising the N x N
+// logits): 3 fp16 MFMAs per fp32 product (hi.hi + hi.lo + lo.hi, 22-bit
+// operands, fp32 accumulation) -- fp32-equivalent results at 16/3 x the fp32
+// matrix rate; logits = M_ij * s_ij / sqrt(C) with M read column-wise (M
+// symmetric => coalesced 128-B rows); incompatible pairs keep logit 0 (not
+// -inf) exactly as :41; online softmax with a lazily re-based running max;
+// split-K over keys when B*N is too small to fill 256 CUs.
+#include "attention_h3.hpp"
 
 namespace pdsc {
 
@@ -73,23 +74,29 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s) {
 }
 
 // ================================================================= attention
-// Production variant of attention.hpp: 4 waves x 32 queries per workgroup,
-// 32-key LDS stages, v_exp_f32 on log2e-prescaled logits, XCD-aware block map
-// (A/B-timed against the other variants with tools/attn_bench.hip).
-constexpr int ATT_NW = 4, ATT_KTS = 32;
+// Production instantiation of attention_h3.hpp: 4 waves x 32 queries per
+// workgroup, XCD-aware block map.  (tools/attn_bench.hip A/B-times it against
+// the exact-fp32-MFMA kernel of attention.hpp.)
+constexpr int ATT_NW = 4;
 
-static AttnGrid prod_grid(int B, int N) { return attention_grid<ATT_NW, ATT_KTS>(B, N, 1024); }
+static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, N, 1024); }
 
 int attention_nsplit(int B, int N) { return prod_grid(B, N).nsplit; }
 
-hipError_t launch_attention(const float *q, const float *k, const float *v, const float *M, int B,
-                            int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s) {
-    const AttnGrid g = prod_grid(B, N);
+hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
+                            int B, int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s) {
+    const AttnGridH3 g = prod_grid(B, N);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
-    const size_t lds = attention_lds_bytes<ATT_NW, ATT_KTS>();
-    auto kern = attention_kernel_t<ATT_NW, ATT_KTS, true, true>;
-    hipLaunchKernelGGL(kern, dim3(g.B * g.nqb * g.nsplit), dim3(ATT_NW * 64), lds, s, q, k, v, M, g,
-                       opart, ml);
+    hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true>), dim3(g.B * g.nqb * g.nsplit), dim3(ATT_NW * 64),
+                       attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
+                            _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s) {
+    const size_t n = (size_t)B * Npad * CH;
+    hipLaunchKernelGGL(split_qkv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, k, v, B, N, ld,
+                       Npad, qs, ks, vs);
     return hipGetLastError();
 }
 
@@ -191,6 +198,86 @@ PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk,
         }
 }
 
+// Q/K/V projections (Conv1d 128 -> 128 + bias, :36-38) of the PT-point tile,
+// written as fp16 hi/lo splits in the attention_h3 layouts.  Wave `ct` owns
+// output channels ct*32..+31 of both 32-point row tiles.
+//   SPLIT_Q, SPLIT_K: transposed product (accumulator rows = channels, lane =
+//     point), so registers 8s..8s+7 are 8 consecutive qk_pos positions: one
+//     16-B store of hi and one of lo per (row tile, s); K chunks swizzled.
+//   SPLIT_V: lane = channel, registers 8s..8s+7 = 8 consecutive v_keypos
+//     positions of the point tile: 16-B stores into the tile's V planes.
+enum SplitMode { SPLIT_Q = 0, SPLIT_K = 1, SPLIT_V = 2 };
+
+template <int MODE>
+PDSC_DEV void dense_split(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, int ct,
+                          _Float16 *__restrict__ dst, int p0, int lane) {
+    const int h = lane >> 5, l32 = lane & 31;
+    f32x16 acc[2] = {zero16(), zero16()};
+    const float *xp = X + l32 * xstr + h * (CH / 2);
+    const f32x4 *wp = reinterpret_cast<const f32x4 *>(pk + off.w) + (size_t)ct * (CH / 8) * 64 + lane;
+    f32x4 wbuf[CH / 8];
+#pragma unroll
+    for (int g = 0; g < CH / 8; ++g) wbuf[g] = wp[g * 64];
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int g = 0; g < CH / 8; ++g) {
+        const f32x4 wb = wbuf[g];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const f32x4 xa = *reinterpret_cast<const f32x4 *>(xp + i * 32 * xstr + 4 * g);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                acc[i] = MODE == SPLIT_V ? mfma32(xa[e], wb[e], acc[i]) : mfma32(wb[e], xa[e], acc[i]);
+        }
+    }
+    if constexpr (MODE == SPLIT_V) {
+        const int c = ct * 32 + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
+        const float bias = pk[off.bias + c];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * (2 * CH * H3_TILE) + rho * H3_TILE;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                f16x8 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    _Float16 a, b;
+                    split_h(acc[i][8 * s + e] + bias, a, b);
+                    hi[e] = a;
+                    lo[e] = b;
+                }
+                const int chk = (2 * s + h) ^ sw;
+                *reinterpret_cast<f16x8 *>(tile + 8 * chk) = hi;
+                *reinterpret_cast<f16x8 *>(tile + CH * H3_TILE + 8 * chk) = lo;
+            }
+        }
+    } else {
+        float bias[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bias[r] = pk[off.bias + ct * 32 + acc_row(r, h)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = p0 + 32 * i + l32;
+            _Float16 *drow = dst + (size_t)row * 2 * CH;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                f16x8 hi, lo;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    _Float16 a, b;
+                    split_h(acc[i][8 * s + e] + bias[8 * s + e], a, b);
+                    hi[e] = a;
+                    lo[e] = b;
+                }
+                int chk = 4 * ct + 2 * s + h;
+                if (MODE == SPLIT_K) chk ^= row & 15;
+                *reinterpret_cast<f16x8 *>(drow + 8 * chk) = hi;
+                *reinterpret_cast<f16x8 *>(drow + CH + 8 * chk) = lo;
+            }
+        }
+    }
+}
+
 template <int IN, int OUT, int EPI>
 PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, float *Y,
                       int ystr, const float *__restrict__ resid, int wave, int lane) {
@@ -225,16 +312,17 @@ struct PwMsg {  // fc_message of one layer
 // until the residual add writes it.
 constexpr size_t PW_LDS = (size_t)(2 * PT * S132) * sizeof(float);
 
-// PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> global); Xout rows -> feat.
+// PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> global split layouts); Xout rows -> feat.
+// Q, K, V point at the pair's buffers.
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
-                      float *__restrict__ feat, float *__restrict__ Q, float *__restrict__ K,
-                      float *__restrict__ V, int p0, int tid, int wave, int lane) {
+                      float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                      _Float16 *__restrict__ V, int p0, int tid, int wave, int lane) {
     dense64<CH, CH, EPI_BN_RELU>(Xin, S132, pk, d.pcn, Xout, S132, nullptr, wave, lane);
     __syncthreads();
     store_rows(Xout, S132, feat, p0, PT, tid);
-    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.q, Q + (size_t)p0 * CH, CH, nullptr, wave, lane);
-    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.k, K + (size_t)p0 * CH, CH, nullptr, wave, lane);
-    dense64<CH, CH, EPI_BIAS>(Xout, S132, pk, d.v, V + (size_t)p0 * CH, CH, nullptr, wave, lane);
+    dense_split<SPLIT_Q>(Xout, S132, pk, d.q, wave, Q, p0, lane);
+    dense_split<SPLIT_K>(Xout, S132, pk, d.k, wave, K, p0, lane);
+    dense_split<SPLIT_V>(Xout, S132, pk, d.v, wave, V, p0, lane);
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
@@ -242,8 +330,8 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
                                                        size_t l0b, PwDense4 d,
                                                        const float *__restrict__ corr, int in_dim,
                                                        int N, int Npad, float *__restrict__ feat,
-                                                       float *__restrict__ Q, float *__restrict__ K,
-                                                       float *__restrict__ V) {
+                                                       _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                                                       _Float16 *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PT * S132, *cp = XB;  // cp: [PT][in_dim], consumed before XB is written
     const int b = blockIdx.y, p0 = blockIdx.x * PT;
@@ -268,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
         XA[p * S132 + j] = s + bj;
     }
     __syncthreads();
-    pcn_qkv(XA, XB, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
+    pcn_qkv(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
@@ -303,8 +391,8 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
                                                      int Npad, float *__restrict__ feat,
-                                                     float *__restrict__ Q, float *__restrict__ K,
-                                                     float *__restrict__ V) {
+                                                     _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                                                     _Float16 *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PT * S132, *XC = XB;
     const int b = blockIdx.y, p0 = blockIdx.x * PT;
@@ -313,7 +401,7 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     combine_tile(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     message_resid(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
-    pcn_qkv(XB, XA, pk, d, feat + boff, Q + boff, K + boff, V + boff, p0, tid, wave, lane);
+    pcn_qkv(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
 __global__ __launch_bounds__(256, 2) void pw_last_kernel(
@@ -369,7 +457,7 @@ static PwDense4 dense4(const LayerOff &l) { return PwDense4{l.pcn, l.q, l.k, l.v
 static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
-                           int N, int Npad, float *feat, float *q, float *k, float *v, hipStream_t s) {
+                           int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v, hipStream_t s) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
     hipLaunchKernelGGL(pw_first_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed, lay.l0_w,
                        lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
@@ -377,8 +465,8 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
 }
 
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, float *q,
-                         float *k, float *v, hipStream_t s) {
+                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, _Float16 *q,
+                         _Float16 *k, _Float16 *v, hipStream_t s) {
     hipLaunchKernelGGL(pw_mid_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed,
                        msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N,
                        Npad, feat, q, k, v);

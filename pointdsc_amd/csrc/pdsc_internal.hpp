@@ -99,18 +99,23 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 
 // Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
 int attention_nsplit(int B, int N);
-hipError_t launch_attention(const float *q, const float *k, const float *v, const float *M, int B,
-                            int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s);
+// q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element).
+hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
+                            int B, int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s);
+// fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
+hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
+                            _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s);
 // Combine partials -> msg [B][Npad][CH] (used by the standalone attention API).
 hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
                                int nsplit, float *msg, hipStream_t s);
 
 // Pointwise chains (one workgroup per PT points).
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
-                           int N, int Npad, float *feat, float *q, float *k, float *v, hipStream_t s);
+                           int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v,
+                           hipStream_t s);
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, float *q,
-                         float *k, float *v, hipStream_t s);
+                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, _Float16 *q,
+                         _Float16 *k, _Float16 *v, hipStream_t s);
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, float *conf, hipStream_t s);
