@@ -105,8 +105,8 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
 }
 
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
-                const Dims &d, const EncBufs &e, float *feat_out, float *normed, float *conf,
-                hipStream_t s) {
+                const Dims &d, const EncBufs &e, float *feat_out, float *normed, _Float16 *normed_s,
+                float *conf, hipStream_t s) {
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
@@ -118,7 +118,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                                  e.k, e.v, s));
         else
             HIPCHK(launch_pw_last(packed, lay, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
-                                  feat_out, normed, conf, s));
+                                  feat_out, normed, normed_s, conf, s));
     }
     return PDSC_OK;
 }
@@ -149,6 +149,7 @@ int run_nsm(const float *normed, const float *src, const float *tgt, const int *
 
 struct FwdBufs {
     float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights, *hsums;
+    _Float16 *normed_s;
     int *seeds, *knn, *counts;
     EncBufs enc;
     NsmBufs nsm;
@@ -159,6 +160,7 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.M = c.take<float>((size_t)d.B * d.N * d.N);
     f.enc = carve_encoder(c, d);
     f.normed = c.take<float>((size_t)d.B * d.N * CH);
+    f.normed_s = c.take<_Float16>((size_t)d.B * d.N * 2 * CH);
     f.conf = c.take<float>((size_t)d.B * d.N);
     f.lm = c.take<float>((size_t)d.B * d.N);
     f.seeds = c.take<int>((size_t)d.B * d.S);
@@ -298,7 +300,7 @@ int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const floa
     Carve c(ws);
     const EncBufs e = carve_encoder(c, d);
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
-    return run_encoder(lay, packed, corr_pos, M, d, e, feat, normed, conf, S_(stream));
+    return run_encoder(lay, packed, corr_pos, M, d, e, feat, normed, nullptr, conf, S_(stream));
 }
 
 size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
@@ -372,7 +374,7 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
 
 // -------------------------------------------------------------------- a6
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S) {
-    return align_bytes((size_t)B * S * N * sizeof(float));
+    return align_bytes((size_t)B * S * N * sizeof(float)) + align_bytes((size_t)B * N * 2 * CH * sizeof(_Float16));
 }
 
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
@@ -383,8 +385,11 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
     if (B < 1 || S < 1 || k < 1 || k + 1 > N || k > 63) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
     RET_IF(need_ws(ws_bytes, pdsc_seed_knn_workspace_bytes(B, N, S)));
     hipStream_t s = S_(stream);
-    float *dist = static_cast<float *>(ws);
-    HIPCHK(launch_knn_dist(normed, seeds, B, N, S, dist, s));
+    Carve c(ws);
+    float *dist = c.take<float>((size_t)B * S * N);
+    _Float16 *ns = c.take<_Float16>((size_t)B * N * 2 * CH);
+    HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
+    HIPCHK(launch_knn_dist(ns, seeds, B, N, S, dist, s));
     HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
     return PDSC_OK;
 }
@@ -487,7 +492,7 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, d, f.enc, nullptr, f.normed, f.conf, s));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s));
@@ -495,7 +500,7 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     STAGE(3);
     // a6 (:250-252)
     HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
-    HIPCHK(launch_knn_dist(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
     HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
     STAGE(4);
     // a7-a8 (:257-282)

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
 
 // fp32 q, k, v [B][ld][CH] (ld >= N rows per pair; rows >= N of the padded
 // layouts become zero) -> Qs, Ks, Vs.  One thread per (pair, row, channel).
-__global__ void split_qkv_kernel(const float *__restrict__ q, const float *__restrict__ k,
+static __global__ void split_qkv_kernel(const float *__restrict__ q, const float *__restrict__ k,
                                  const float *__restrict__ v, int B, int N, int ld, int Npad,
                                  _Float16 *__restrict__ Qs, _Float16 *__restrict__ Ks,
                                  _Float16 *__restrict__ Vs) {

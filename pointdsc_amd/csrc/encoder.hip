@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
     const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
     const float *__restrict__ feat, float *__restrict__ feat_out, float *__restrict__ normed,
-    float *__restrict__ conf) {
+    _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PT * S132, *XC = XB;
     float *C1 = XA, *C2 = XA + PT * S36;  // classifier hidden layers reuse A
@@ -439,6 +439,22 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
                 *reinterpret_cast<f32x4 *>(dst + 4 * i) =
                     f32x4{XB[p * S132 + d0 + 4 * i] / den, XB[p * S132 + d0 + 4 * i + 1] / den,
                           XB[p * S132 + d0 + 4 * i + 2] / den, XB[p * S132 + d0 + 4 * i + 3] / den};
+            if (normed_s) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
+                _Float16 *ds = normed_s + ((size_t)b * N + p0 + p) * 2 * CH;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f16x8 hi, lo;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        _Float16 a, c;
+                        split_h(XB[p * S132 + qk_pos(d0 + 8 * q + e)] / den, a, c);
+                        hi[e] = a;
+                        lo[e] = c;
+                    }
+                    *reinterpret_cast<f16x8 *>(ds + d0 + 8 * q) = hi;
+                    *reinterpret_cast<f16x8 *>(ds + CH + d0 + 8 * q) = lo;
+                }
+            }
         }
     }
     // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171)
@@ -475,10 +491,10 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
 
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
-                          float *feat_out, float *normed, float *conf, hipStream_t s) {
+                          float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s) {
     hipLaunchKernelGGL(pw_last_kernel, dim3((N + PT - 1) / PT, B), dim3(256), PW_LDS, s, packed,
                        msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml,
-                       nsplit, N, Npad, feat, feat_out, normed, conf);
+                       nsplit, N, Npad, feat, feat_out, normed, normed_s, conf);
     return hipGetLastError();
 }
 

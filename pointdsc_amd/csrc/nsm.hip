@@ -1,9 +1,10 @@
 // nsm.hip -- a6-a11: Neural Spectral Matching, hypothesis verification and
 // post-refinement.
 //
-//   knn_dist     a6  seed rows of 2 - 2 F F^T (v_mfma_f32_32x32x2_f32), [B][S][N]
-//   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed):
-//                    4-pass 8-bit radix select + ordered ballot compaction
+//   knn_dist     a6  seed rows of 2 - 2 F F^T (3-product fp16 MFMA), [B][S][N]
+//   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed,
+//                    row in registers): 8-bit radix select from the highest
+//                    differing bit + ordered ballot compaction
 //   nsm_local    a7  gather k neighbours, k x k feature*spatial consistency T
 //   nsm_iter     a8  all num_iterations power iterates + per-iterate allclose flags
 //   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
@@ -12,58 +13,83 @@
 //                    inlier count over all N correspondences
 //   select_best  a10 first argmax of fitness, labels of the best hypothesis
 //   post_refine  a11 <= 20 device-side IRLS refits, one workgroup per pair
-#include "pdsc_internal.hpp"
+#include "attention_h3.hpp"
 
 namespace pdsc {
 
 // ------------------------------------------------------------------ a6 kNN
 // dist[b][s][j] = 2 - 2 * <normed[seed_s], normed[j]>   (models/common.py:58-60)
-__global__ __launch_bounds__(256) void knn_dist_kernel(const float *__restrict__ normed,
+// on the fp16 matrix cores with the 3-product split of attention_h3.hpp
+// (|error| <= 2^-21 on a distance in [0, 4], i.e. fp32-equivalent): ns is the
+// split copy of normed, [B][N][2][128] fp16 in qk_pos order (pw_last writes it).
+// A wave = 32 seeds (lane <-> seed fragment, held in registers) x KPW tiles
+// of 32 keys (lane <-> key: the accumulator register r is seed row
+// acc_row(r, h), so each store instruction writes 128 contiguous bytes).
+constexpr int KNN_KPW = 2;
+
+__global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
                                                        const int *__restrict__ seeds, int N, int S,
                                                        float *__restrict__ dist) {
-    const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.z, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, l32 = lane & 31;
-    const int s0 = blockIdx.y * 32, j0 = blockIdx.x * 128 + wave * 32;
-    const float *F = normed + (size_t)b * N * CH;
+    const int s0 = blockIdx.y * 32;
+    const _Float16 *F = ns + (size_t)b * N * 2 * CH;
     const int sidx = s0 + l32;
-    const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : -1;
-    float af[64];
+    const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
+    f16x8 ah[8], al[8];
     {
-        const f32x4 *src4 = reinterpret_cast<const f32x4 *>(F + (size_t)max(seed, 0) * CH + h * 64);
+        const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            f32x4 t = src4[i];
-            if (seed < 0) t = f32x4{0, 0, 0, 0};
-            af[4 * i] = t[0];
-            af[4 * i + 1] = t[1];
-            af[4 * i + 2] = t[2];
-            af[4 * i + 3] = t[3];
+        for (int j = 0; j < 8; ++j) {
+            ah[j] = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * j + h));
+            al[j] = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * j + h));
         }
     }
-    const int j = j0 + l32;
-    const f32x4 *bp = reinterpret_cast<const f32x4 *>(F + (size_t)min(j, N - 1) * CH + h * 64);
-    f32x16 acc = zero16();
+    for (int kt = 0; kt < KNN_KPW; ++kt) {
+        const int j0 = ((blockIdx.x * 4 + wave) * KNN_KPW + kt) * 32;
+        if (j0 >= N) break;  // wave-uniform
+        const int j = j0 + l32;
+        const char *row = reinterpret_cast<const char *>(F + (size_t)min(j, N - 1) * 2 * CH);
+        f32x16 acc = zero16();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const f32x4 bv = bp[i];
-        acc = mfma32(af[4 * i], bv[0], acc);
-        acc = mfma32(af[4 * i + 1], bv[1], acc);
-        acc = mfma32(af[4 * i + 2], bv[2], acc);
-        acc = mfma32(af[4 * i + 3], bv[3], acc);
-    }
-    if (j < N) {
+        for (int i = 0; i < 8; ++i) {
+            const f16x8 bh = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * i + h));
+            const f16x8 bl = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * i + h));
+            acc = mfma_h3(ah[i], al[i], bh, bl, acc);
+        }
+        if (j < N) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int s = s0 + acc_row(r, h);
-            if (s < S) dist[((size_t)b * S + s) * N + j] = 2.0f - 2.0f * acc[r];
+            for (int r = 0; r < 16; ++r) {
+                const int s = s0 + acc_row(r, h);
+                if (s < S) dist[((size_t)b * S + s) * N + j] = 2.0f - 2.0f * acc[r];
+            }
         }
     }
 }
 
-hipError_t launch_knn_dist(const float *normed, const int *seeds, int B, int N, int S, float *dist,
+hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s) {
-    hipLaunchKernelGGL(knn_dist_kernel, dim3((N + 127) / 128, (S + 31) / 32, B), dim3(256), 0, s,
-                       normed, seeds, N, S, dist);
+    const int per_block = 4 * KNN_KPW * 32;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3((N + per_block - 1) / per_block, (S + 31) / 32, B), dim3(256), 0, s,
+                       ns, seeds, N, S, dist);
+    return hipGetLastError();
+}
+
+// fp32 rows [rows][128] -> [rows][2][128] fp16 hi/lo in qk_pos order (standalone API)
+__global__ void split_rows_kernel(const float *__restrict__ x, size_t rows, _Float16 *__restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * CH) return;
+    const size_t row = i / CH;
+    const int c = (int)(i % CH);
+    _Float16 hi, lo;
+    split_h(x[i], hi, lo);
+    out[qs_off((int)0, 0, c) + row * 2 * CH] = hi;
+    out[qs_off((int)0, 1, c) + row * 2 * CH] = lo;
+}
+
+hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s) {
+    const size_t n = rows * CH;
+    hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, rows, out);
     return hipGetLastError();
 }
 
@@ -74,12 +100,18 @@ PDSC_DEV uint32_t fkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// topk(k+1, smallest) of one seed row, one WAVE per seed (4 per workgroup):
-// four 8-bit radix passes find the (k+1)-th smallest key T exactly (per-wave
-// LDS histogram, shuffle scan); one ordered pass then collects every key < T
-// and the first `need` keys == T in index order (ballot + popcount
-// compaction); the k+1 candidates are ranked by (key, index) and the first is
-// dropped positionally (models/common.py:68).  k + 1 <= 64.
+// topk(k+1, smallest) of one seed row, one WAVE per seed (4 per workgroup).
+// The row's keys live in registers (R per lane, R*64 >= N; R = 0: re-read
+// from memory each pass, any N).  Radix select on the order-preserving keys:
+// starting at the highest bit where the row's min and max keys differ (the
+// common prefix carries no information -- distances in [0, 4] share their top
+// byte, and an 8-bit digit there would put every key in one histogram bin),
+// 8-bit digits are histogrammed in LDS until the bin holding the (k+1)-th
+// smallest key is taken whole or the key is resolved.  One ordered pass then
+// collects every key below that bin and the first `need` keys of it in index
+// order (ballot + popcount compaction); the k+1 candidates are ranked by
+// (key, index) and the first is dropped positionally (models/common.py:68).
+template <int R>
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int N, int S,
                                                          int k, int *__restrict__ knn) {
     __shared__ uint32_t hist[4][256];
@@ -89,59 +121,107 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     const int s = blockIdx.x * 4 + wave;
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
     const float *row = dist + ((size_t)b * S + s) * N;
-    uint32_t *h = hist[wave];
+    // NI chunks of 64 keys: compile-time (fully unrolled, registers) or runtime (memory)
+    const int NI = R > 0 ? R : (N + 63) / 64;
+    uint32_t key[R > 0 ? R : 1];
+    if constexpr (R > 0) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int j = lane + 64 * i;
+            key[i] = j < N ? fkey(row[j]) : 0xffffffffu;
+        }
+    }
+    // key of chunk i for this lane (0xffffffff past the end: never selected)
+    auto K = [&](int i) -> uint32_t {
+        if constexpr (R > 0) {
+            return key[i];
+        } else {
+            const int j = lane + 64 * i;
+            return j < N ? fkey(row[j]) : 0xffffffffu;
+        }
+    };
+    uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        if (lane + 64 * i < N) {
+            const uint32_t u = K(i);
+            kmin = min(kmin, u);
+            kmax = max(kmax, u);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    uint32_t *hb = hist[wave];
     const uint32_t want = k + 1;
-    uint32_t need = want, prefix = 0, mask = 0;
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = 24 - 8 * pass;
+    uint32_t need = want, prefix = kmin, mask = 0xffffffffu;
+    if (kmin != kmax) {
+        const int top = 31 - __clz((int)(kmin ^ kmax));  // highest differing bit
+        mask = top == 31 ? 0u : ~((2u << top) - 1u);
+        prefix = kmin & mask;
+        for (int hi = top; hi >= 0; hi -= 8) {
+            const int lo = max(hi - 7, 0);
+            const uint32_t dm = (2u << (hi - lo)) - 1u;  // digit = bits [lo, hi]
 #pragma unroll
-        for (int e = 0; e < 4; ++e) h[lane + 64 * e] = 0;
-        __builtin_amdgcn_wave_barrier();
-        for (int j = lane; j < N; j += 64) {
-            const uint32_t u = fkey(row[j]);
-            if ((u & mask) == prefix) atomicAdd(&h[(u >> shift) & 255u], 1u);
-        }
-        __builtin_amdgcn_wave_barrier();
-        uint32_t c[4], tot = 0;
+            for (int e = 0; e < 4; ++e) hb[lane + 64 * e] = 0;
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            c[e] = h[4 * lane + e];
-            tot += c[e];
-        }
-        uint32_t incl = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
-        }
-        const uint32_t base = incl - tot;
-        uint32_t my_bin = 0, my_need = 0;
-        const bool hit = base < need && need <= incl;
-        if (hit) {
-            uint32_t cum = base;
+            for (int i = 0; i < NI; ++i) {
+                const uint32_t u = K(i);
+                if (lane + 64 * i < N && (u & mask) == prefix) atomicAdd(&hb[(u >> lo) & dm], 1u);
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint32_t c[4], tot = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                if (my_need == 0 && cum + c[e] >= need) {
-                    my_bin = 4 * lane + e;
-                    my_need = need - cum;
-                }
-                cum += c[e];
+                c[e] = hb[4 * lane + e];
+                tot += c[e];
             }
+            uint32_t incl = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            const uint32_t base = incl - tot;
+            uint32_t my_bin = 0, my_need = 0, my_cnt = 0;
+            const bool hit = base < need && need <= incl;
+            if (hit) {
+                uint32_t cum = base;
+                bool done = false;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (!done && cum + c[e] >= need) {
+                        my_bin = 4 * lane + e;
+                        my_need = need - cum;
+                        my_cnt = c[e];
+                        done = true;
+                    }
+                    cum += c[e];
+                }
+            }
+            const int src_lane = __ffsll((unsigned long long)__ballot(hit)) - 1;
+            const uint32_t bin = __shfl(my_bin, src_lane);
+            const uint32_t cnt = __shfl(my_cnt, src_lane);
+            need = __shfl(my_need, src_lane);
+            prefix |= bin << lo;
+            mask |= dm << lo;
+            if (cnt == need) break;  // the whole bin is taken: no need to resolve further
         }
-        const int src_lane = __ffsll((unsigned long long)__ballot(hit)) - 1;
-        const uint32_t bin = __shfl(my_bin, src_lane);
-        need = __shfl(my_need, src_lane);
-        prefix |= bin << shift;
-        mask |= 255u << shift;
     }
-    // prefix = T: take all keys < T and the `need` lowest-index keys == T, in index order
+    // take every key with (u & mask) < prefix and the first `need` keys with (u & mask) == prefix
     const uint32_t nless = want - need;
     const unsigned long long below = (1ull << lane) - 1ull;
     uint32_t pl = 0, pe = 0;
-    for (int j0 = 0; j0 < N && (pl < nless || pe < need); j0 += 64) {
-        const int j = j0 + lane;
-        const uint32_t u = (j < N) ? fkey(row[j]) : 0xffffffffu;
-        const bool less = j < N && u < prefix, eq = j < N && u == prefix;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int j = lane + 64 * i;
+        const uint32_t u = K(i);
+        const uint32_t um = u & mask;
+        const bool valid = j < N;
+        const bool less = valid && um < prefix, eq = valid && um == prefix;
         const unsigned long long lm = __ballot(less), em = __ballot(eq);
         if (less) {
             const uint32_t pos = pl + __popcll(lm & below);
@@ -174,7 +254,24 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
 }
 
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s) {
-    hipLaunchKernelGGL(knn_select_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, dist, N, S, k, knn);
+    const dim3 grid((S + 3) / 4, B);
+    const int R = (N + 63) / 64;
+    if (R <= 16)
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 32)
+        hipLaunchKernelGGL(knn_select_kernel<32>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 48)
+        hipLaunchKernelGGL(knn_select_kernel<48>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 64)
+        hipLaunchKernelGGL(knn_select_kernel<64>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 80)
+        hipLaunchKernelGGL(knn_select_kernel<80>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 96)
+        hipLaunchKernelGGL(knn_select_kernel<96>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else if (R <= 128)
+        hipLaunchKernelGGL(knn_select_kernel<128>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+    else
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), 0, s, dist, N, S, k, knn);
     return hipGetLastError();
 }
 

@@ -118,15 +118,17 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
                          _Float16 *k, _Float16 *v, hipStream_t s);
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
-                          float *feat_out, float *normed, float *conf, hipStream_t s);
+                          float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s);
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s);
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
                             hipStream_t s);
 
-hipError_t launch_knn_dist(const float *normed, const int *seeds, int B, int N, int S, float *dist,
+// ns: normed as [B][N][2][128] fp16 hi/lo (qk_pos order, attention_h3.hpp)
+hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s);
+hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s);
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s);
 // Tg: scratch [B][S][k][k]
 hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
