@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "pdsc_internal.hpp"
@@ -54,6 +55,15 @@ struct Carve {
         return p;
     }
 };
+
+// A/B knob (measurement only): PDSC_DENSE_M=1 makes the forward write and read M dense.
+bool dense_m_requested() {
+    static const bool v = [] {
+        const char *e = getenv("PDSC_DENSE_M");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 
 int check_cfg(const pdsc_config *cfg) {
     if (!cfg) return fail(PDSC_ERR_ARG, "cfg is NULL");
@@ -105,13 +115,13 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
 }
 
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
-                const Dims &d, const EncBufs &e, float *feat_out, float *normed, _Float16 *normed_s,
-                float *conf, hipStream_t s) {
+                bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
+                _Float16 *normed_s, float *conf, hipStream_t s) {
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
-        HIPCHK(launch_attention(e.q, e.k, e.v, M, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        HIPCHK(launch_attention(e.q, e.k, e.v, M, m_packed, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         if (l + 1 < lay.L)
             HIPCHK(launch_pw_mid(packed, lay, l, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
@@ -157,7 +167,8 @@ struct FwdBufs {
 
 FwdBufs carve_forward(Carve &c, const Dims &d) {
     FwdBufs f;
-    f.M = c.take<float>((size_t)d.B * d.N * d.N);
+    // symmetric-packed tiles (PDSC_DENSE_M=1: the dense [N][N] form, for A/B measurement)
+    f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), (size_t)d.N * d.N));
     f.enc = carve_encoder(c, d);
     f.normed = c.take<float>((size_t)d.B * d.N * CH);
     f.normed_s = c.take<_Float16>((size_t)d.B * d.N * 2 * CH);
@@ -300,7 +311,7 @@ int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const floa
     Carve c(ws);
     const EncBufs e = carve_encoder(c, d);
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
-    return run_encoder(lay, packed, corr_pos, M, d, e, feat, normed, nullptr, conf, S_(stream));
+    return run_encoder(lay, packed, corr_pos, M, false, d, e, feat, normed, nullptr, conf, S_(stream));
 }
 
 size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
@@ -330,7 +341,7 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     float *ml = c.take<float>((size_t)B * Npad * ns * 2);
     // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
     HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, s));
-    HIPCHK(launch_attention(qs, ks, vs, M, B, N, Npad, ns, op, ml, s));
+    HIPCHK(launch_attention(qs, ks, vs, M, false, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
@@ -489,10 +500,14 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     if (ev) HIPCHK(hipEventRecord(ev[i], s))
     STAGE(0);
     // a1 (:150-153)
-    HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    const bool mpacked = !dense_m_requested();
+    if (mpacked)
+        HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    else
+        HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s));

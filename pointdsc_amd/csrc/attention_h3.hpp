@@ -111,7 +111,8 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
     return g;
 }
 
-template <int NW, bool XCD>
+// PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
+template <int NW, bool XCD, bool PACKED>
 __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart, float *__restrict__ ml) {
@@ -137,7 +138,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
 
     const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
     const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
-    const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M + (size_t)b * N * N, (uint32_t)N * (uint32_t)N * 4u);
+    const int mnt = mpack_ntile(N);
+    const size_t mper = PACKED ? (size_t)mnt * (mnt + 1) / 2 * MPACK_T * MPACK_T : (size_t)N * N;
+    const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M + (size_t)b * mper, (uint32_t)(mper * 4u));
 
     // this lane's query: 8 k-steps x (hi, lo) fragments, chunk 2j + h of its row
     f16x8 qh[8], ql[8];
@@ -172,11 +175,36 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     auto tile = [&](const char *Kl, const char *Vl, int key0) {
         // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys, issued first
         float mv[16];
-        const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
+        if constexpr (PACKED) {
+            // the wave's 32 x 32 block IS one packed tile: (kt, qt) row-major when
+            // kt <= qt, else tile (qt, kt) read transposed (wave-uniform branch)
+            static_assert(MPACK_T == 32, "one packed tile per wave step");
+            const int kt = key0 / MPACK_T, qt = q0 / MPACK_T;
+            const int kr = 4 * h, qr = l32;
+            if (kt <= qt) {  // rows = keys: 16 loads, each 32 consecutive queries of a key row
+                const uint32_t vo =
+                    ((uint32_t)mpack_tile(kt, qt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(kr * MPACK_T + qr)) * 4;
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            mv[r] = __builtin_bit_cast(
-                float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb, 0, 0));
+                for (int r = 0; r < 16; ++r)
+                    mv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                          rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * (MPACK_T * 4), 0, 0));
+            } else {  // rows = queries: the lane's 16 keys are 4 runs of 4 in its query's row
+                const uint32_t vo =
+                    ((uint32_t)mpack_tile(qt, kt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(qr * MPACK_T + kr)) * 4;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM, vo + 32 * g, 0, 0));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[e];
+                }
+            }
+        } else {
+            const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                mv[r] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb, 0, 0));
+        }
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
         const char *krow = Kl + l32 * H3_ROWB;

@@ -15,7 +15,30 @@
 
 namespace pdsc {
 
-constexpr int CT = 64;  // tile edge
+constexpr int CT = 64;  // tile edge (dense kernel)
+
+// Correctly rounded sqrtf for x == 0, +inf or x >= 2^-96 (the caller takes
+// the library sqrtf when a wave holds a smaller positive x): v_sqrt_f32 is
+// within 1 ulp, and the neighbour whose fma residual shows it closer replaces
+// it -- the same correction hipcc's -fhip-fp32-correctly-rounded-divide-sqrt
+// emits, minus the denormal rescaling and class fix-ups this domain needs not.
+PDSC_DEV float cr_sqrt(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(s) - 1u), up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-dn, s, x), rup = __builtin_fmaf(-up, s, x);
+    float r = rdn <= 0.0f ? dn : s;
+    r = rup > 0.0f ? up : r;
+    return x == 0.0f ? x : r;
+}
+
+// Correctly rounded x / d given rcp = RN(1/d) (Markstein: q = RN(x rcp) is
+// within 1 ulp, the fma remainder is exact, and one fma correction rounds
+// to RN(x / d); x, d normal and no overflow -- d = sigma_d^2 > 0).
+PDSC_DEV float cr_div(float x, float d, float rcp) {
+    const float q = x * rcp;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
 
 __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ src,
                                                      const float *__restrict__ tgt, int N,
@@ -30,6 +53,10 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
     const int b = blockIdx.y;
     const float sd = sigma_d_ptr[0];
     const float s2 = sd * sd;
+    const float rs2 = 1.0f / s2;  // correctly rounded (the library division)
+    // fast path: every squared distance of the tile is 0 or >= 2^-96 and s2 is a normal
+    // number with a normal reciprocal (checked per element below, wave-uniformly)
+    const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
     src += (size_t)b * N * 3;
     tgt += (size_t)b * N * 3;
     M += (size_t)b * N * N;
@@ -53,16 +80,32 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
         const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
         const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
         float out[4];
+        float xs[4], xt[4];
+        bool tiny = false;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int c = cq * 4 + q;
-            const float ds = pdist3(six, siy, siz, pts[2][c][0], pts[2][c][1], pts[2][c][2]);
-            const float dt = pdist3(tix, tiy, tiz, pts[3][c][0], pts[3][c][1], pts[3][c][2]);
-            const float d = ds - dt;
-            const float m = 1.0f - (d * d) / s2;
-            out[q] = m > 0.0f ? m : 0.0f;
-            tileT[c][r] = out[q];
+            xs[q] = sqdist3(six, siy, siz, pts[2][c][0], pts[2][c][1], pts[2][c][2]);
+            xt[q] = sqdist3(tix, tiy, tiz, pts[3][c][0], pts[3][c][1], pts[3][c][2]);
+            tiny |= (xs[q] != 0.0f && !(xs[q] >= 0x1p-96f)) || (xt[q] != 0.0f && !(xt[q] >= 0x1p-96f));
         }
+        if (s2ok && !__any(tiny)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = cr_sqrt(xs[q]) - cr_sqrt(xt[q]);
+                const float m = 1.0f - cr_div(d * d, s2, rs2);
+                out[q] = m > 0.0f ? m : 0.0f;
+            }
+        } else {  // library sqrtf and '/' (correctly rounded in every case)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = sqrtf(xs[q]) - sqrtf(xt[q]);
+                const float m = 1.0f - (d * d) / s2;
+                out[q] = m > 0.0f ? m : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tileT[cq * 4 + q][r] = out[q];
         if (i < N) {
             const int j = j0 + cq * 4;
             float *dst = M + (size_t)i * N + j;
@@ -93,6 +136,91 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
                 if (j + q < N) dst[q] = o[q];
         }
     }
+}
+
+// The forward's M: symmetric-packed 32 x 32 tiles (pdsc_internal.hpp,
+// mpack_tile), each one contiguous 4 KiB block -- half the bytes of the dense
+// matrix, and each block exactly the 32 keys x 32 queries an attention wave
+// reads per step (in either orientation).  A workgroup computes a 64 x 64
+// upper-triangle block (ti <= tj) like the dense kernel and stores its four
+// 32 x 32 tiles (three on the diagonal: the lower one is the transpose of the
+// upper).  (The dense, twice-written form above costs 2x the bytes in 256-B
+// segments strided by 4N B: ~2.9 TB/s at N = 5000 against ~5.3 TB/s for
+// contiguous stores, tools/compat_bench.hip.)  Entries past N are written as 0.
+__global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restrict__ src,
+                                                            const float *__restrict__ tgt, int N, int ntile,
+                                                            const float *__restrict__ sigma_d_ptr,
+                                                            float *__restrict__ Mp) {
+    __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
+    int t = blockIdx.x, ti = 0;
+    while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
+    const int tj = ti + t;
+    const int b = blockIdx.y;
+    const float sd = sigma_d_ptr[0];
+    const float s2 = sd * sd;
+    const float rs2 = 1.0f / s2;
+    const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
+    src += (size_t)b * N * 3;
+    tgt += (size_t)b * N * 3;
+    const int nt32 = mpack_ntile(N);
+    float *Mb = Mp + (size_t)b * mpack_floats(N);
+    const int tid = threadIdx.x;
+    const int i0 = ti * CT, j0 = tj * CT;
+    for (int e = tid; e < CT * 3; e += 256) {
+        const int p = e / 3, c = e % 3;
+        pts[0][p][c] = (i0 + p < N) ? src[(size_t)(i0 + p) * 3 + c] : 0.f;
+        pts[1][p][c] = (i0 + p < N) ? tgt[(size_t)(i0 + p) * 3 + c] : 0.f;
+        pts[2][p][c] = (j0 + p < N) ? src[(size_t)(j0 + p) * 3 + c] : 0.f;
+        pts[3][p][c] = (j0 + p < N) ? tgt[(size_t)(j0 + p) * 3 + c] : 0.f;
+    }
+    __syncthreads();
+    const int cq = tid & 15, rq = tid >> 4;
+    const int tc = 2 * tj + (cq >> 3);  // the 32-tile column of this thread's 4 columns
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+        const int r = rq + 16 * rr;
+        const int tr = 2 * ti + (r >> 5);
+        if (tr > tc || tr >= nt32 || tc >= nt32) continue;  // below the diagonal (diagonal block) / past N
+        const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
+        const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
+        float xs[4], xt[4], out[4];
+        bool tiny = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = cq * 4 + q;
+            xs[q] = sqdist3(six, siy, siz, pts[2][c][0], pts[2][c][1], pts[2][c][2]);
+            xt[q] = sqdist3(tix, tiy, tiz, pts[3][c][0], pts[3][c][1], pts[3][c][2]);
+            tiny |= (xs[q] != 0.0f && !(xs[q] >= 0x1p-96f)) || (xt[q] != 0.0f && !(xt[q] >= 0x1p-96f));
+        }
+        if (s2ok && !__any(tiny)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = cr_sqrt(xs[q]) - cr_sqrt(xt[q]);
+                const float m = 1.0f - cr_div(d * d, s2, rs2);
+                out[q] = m > 0.0f ? m : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = sqrtf(xs[q]) - sqrtf(xt[q]);
+                const float m = 1.0f - (d * d) / s2;
+                out[q] = m > 0.0f ? m : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (i0 + r >= N || j0 + cq * 4 + q >= N) out[q] = 0.0f;
+        float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
+        *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{out[0], out[1], out[2], out[3]};
+    }
+}
+
+hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
+                                float *Mp, hipStream_t stream) {
+    const int ntile = (N + CT - 1) / CT;  // 64-point compute blocks
+    const int ntri = ntile * (ntile + 1) / 2;
+    hipLaunchKernelGGL(compat_packed_kernel, dim3(ntri, B), dim3(256), 0, stream, src, tgt, N, ntile, sigma_d, Mp);
+    return hipGetLastError();
 }
 
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,

@@ -84,11 +84,16 @@ static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, 
 int attention_nsplit(int B, int N) { return prod_grid(B, N).nsplit; }
 
 hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
-                            int B, int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s) {
+                            bool m_packed, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+                            hipStream_t s) {
     const AttnGridH3 g = prod_grid(B, N);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true>), dim3(g.B * g.nqb * g.nsplit), dim3(ATT_NW * 64),
-                       attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+    if (m_packed)
+        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), dim3(g.B * g.nqb * g.nsplit),
+                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+    else
+        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), dim3(g.B * g.nqb * g.nsplit),
+                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
     return hipGetLastError();
 }
 

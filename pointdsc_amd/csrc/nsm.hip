@@ -107,16 +107,22 @@ PDSC_DEV uint32_t fkey(float f) {
 // common prefix carries no information -- distances in [0, 4] share their top
 // byte, and an 8-bit digit there would put every key in one histogram bin),
 // 8-bit digits are histogrammed in LDS until the bin holding the (k+1)-th
-// smallest key is taken whole or the key is resolved.  One ordered pass then
-// collects every key below that bin and the first `need` keys of it in index
-// order (ballot + popcount compaction); the k+1 candidates are ranked by
-// (key, index) and the first is dropped positionally (models/common.py:68).
+// smallest key is taken whole, holds <= KNN_BINCAP keys, or the key is
+// resolved.  One ordered pass then collects every key below that bin (ballot
+// + popcount compaction) and either the bin's keys (ranked by (key, index) to
+// pick the `need` smallest -- usually after ONE histogram pass) or its first
+// `need` keys in index order; the k+1 candidates are ranked by (key, index)
+// and the first is dropped positionally (models/common.py:68).
+constexpr int KNN_BINCAP = 64;
+
 template <int R>
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int N, int S,
                                                          int k, int *__restrict__ knn) {
     __shared__ uint32_t hist[4][256];
     __shared__ uint32_t ckey[4][64];
     __shared__ int cidx[4][64];
+    __shared__ uint32_t bkey[4][KNN_BINCAP];
+    __shared__ int bidx[4][KNN_BINCAP];
     const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s = blockIdx.x * 4 + wave;
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
@@ -156,7 +162,8 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     }
     uint32_t *hb = hist[wave];
     const uint32_t want = k + 1;
-    uint32_t need = want, prefix = kmin, mask = 0xffffffffu;
+    uint32_t need = want, prefix = kmin, mask = 0xffffffffu, bin_cnt = want;
+    bool small_bin = false;  // the bin holding the (k+1)-th key has <= KNN_BINCAP keys: rank them directly
     if (kmin != kmax) {
         const int top = 31 - __clz((int)(kmin ^ kmax));  // highest differing bit
         mask = top == 31 ? 0u : ~((2u << top) - 1u);
@@ -208,7 +215,12 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             need = __shfl(my_need, src_lane);
             prefix |= bin << lo;
             mask |= dm << lo;
+            bin_cnt = cnt;
             if (cnt == need) break;  // the whole bin is taken: no need to resolve further
+            if (cnt <= KNN_BINCAP) {
+                small_bin = true;
+                break;
+            }
         }
     }
     // take every key with (u & mask) < prefix and the first `need` keys with (u & mask) == prefix
@@ -232,7 +244,10 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         }
         if (eq) {
             const uint32_t r = pe + __popcll(em & below);
-            if (r < need) {
+            if (small_bin) {  // every key of the bin, ranked below
+                bkey[wave][r] = u;
+                bidx[wave][r] = j;
+            } else if (r < need) {
                 ckey[wave][nless + r] = u;
                 cidx[wave][nless + r] = j;
             }
@@ -241,6 +256,22 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         pe += __popcll(em);
     }
     __builtin_amdgcn_wave_barrier();
+    if (small_bin) {  // the `need` smallest (key, index) of the bin's bin_cnt keys
+        for (int e = lane; e < (int)bin_cnt; e += 64) {
+            const uint32_t ku = bkey[wave][e];
+            const int ki = bidx[wave][e];
+            uint32_t rank = 0;
+            for (int m = 0; m < (int)bin_cnt; ++m) {
+                const uint32_t mu = bkey[wave][m];
+                rank += (mu < ku) || (mu == ku && bidx[wave][m] < ki);
+            }
+            if (rank < need) {
+                ckey[wave][nless + rank] = ku;
+                cidx[wave][nless + rank] = ki;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
     if (lane < (int)want) {
         const uint32_t ku = ckey[wave][lane];
         const int ki = cidx[wave][lane];
@@ -538,7 +569,7 @@ __global__ __launch_bounds__(64) void kabsch_solve_kernel(const float *__restric
 __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restrict__ src,
                                                             const float *__restrict__ tgt,
                                                             const float *__restrict__ seed_trans,
-                                                            int N, int S, float tau,
+                                                            int N, int S, float tau2,
                                                             int *__restrict__ counts) {
     __shared__ float Ts[HS][12];
     __shared__ int wc[4][HS];
@@ -557,7 +588,7 @@ __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restr
         const float x = sb[3 * n], y = sb[3 * n + 1], z = sb[3 * n + 2];
         const float tx = tb[3 * n], ty = tb[3 * n + 1], tz = tb[3 * n + 2];
 #pragma unroll
-        for (int q = 0; q < HS; ++q) c[q] += residual(Ts[q], x, y, z, tx, ty, tz) < tau;  // (:327-328)
+        for (int q = 0; q < HS; ++q) c[q] += residual_sq(Ts[q], x, y, z, tx, ty, tz) < tau2;  // L2 < tau (:327-328)
     }
 #pragma unroll
     for (int q = 0; q < HS; ++q) {
@@ -576,7 +607,7 @@ hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn,
     const int n = B * S;
     hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, seed_trans);
     hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
-                       seed_trans, N, S, tau, counts);
+                       seed_trans, N, S, sqrt_ge_threshold(tau), counts);
     return hipGetLastError();
 }
 

@@ -39,6 +39,25 @@ PDSC_DEV float pdist3(float ax, float ay, float az, float bx, float by, float bz
     return sqrtf(__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));
 }
 
+// The squared norm under pdist3's sqrtf (models/PointDSC.py:151-152 order).
+PDSC_DEV float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+// Comparisons against a correctly rounded square root without taking it:
+// sqrtf is monotone, so for the smallest float t with sqrtf(t) >= R,
+//   sqrtf(x) >= R  <=>  x >= t      and      sqrtf(x) < R  <=>  x < t
+// for every x (NaN included: both sides false).  Host-side, IEEE sqrtf.
+inline float sqrt_ge_threshold(float R) {
+    if (R != R) return R;            // NaN: every comparison false, as with sqrtf(x) >= NaN
+    if (R <= 0.0f) return 0.0f;      // sqrtf(x) >= R for every x >= 0
+    float t = R * R;
+    while (t > 0.0f && sqrtf(__builtin_nextafterf(t, 0.0f)) >= R) t = __builtin_nextafterf(t, 0.0f);
+    while (sqrtf(t) < R) t = __builtin_nextafterf(t, __builtin_inff());
+    return t;
+}
+
 // |v| for a residual vector, same evaluation order as pdist3.
 PDSC_DEV float norm3(float dx, float dy, float dz) {
     return sqrtf(__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));
@@ -62,6 +81,14 @@ PDSC_DEV float residual(const float *T, float x, float y, float z, float tx, flo
     const float py = (T[4] * x + T[5] * y) + T[6] * z + T[7];
     const float pz = (T[8] * x + T[9] * y) + T[10] * z + T[11];
     return norm3(px - tx, py - ty, pz - tz);
+}
+// residual()^2 before its sqrtf: residual(...) < tau  <=>  residual_sq(...) < sqrt_ge_threshold(tau)
+PDSC_DEV float residual_sq(const float *T, float x, float y, float z, float tx, float ty, float tz) {
+    const float px = (T[0] * x + T[1] * y) + T[2] * z + T[3];
+    const float py = (T[4] * x + T[5] * y) + T[6] * z + T[7];
+    const float pz = (T[8] * x + T[9] * y) + T[10] * z + T[11];
+    const float dx = px - tx, dy = py - ty, dz = pz - tz;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
 }
 
 // ---------------------------------------------------------------------------

@@ -14,6 +14,19 @@ constexpr int KT = 32;        // keys per attention tile
 constexpr int PT = 64;        // points per pointwise workgroup
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ---- symmetric-packed M (the forward's a1 output) -------------------------
+// M is symmetric bit-for-bit, so the forward stores only its upper-triangle
+// MPACK_T x MPACK_T tiles, each contiguous and row-major, enumerated row by
+// row: tile (ti, tj), ti <= tj, at index ti*nt - ti*(ti-1)/2 + (tj - ti),
+// nt = ceil(N / MPACK_T).  M[i][j] for i > j lives transposed in tile (tj, ti).
+constexpr int MPACK_T = 32;  // = the attention's per-wave 32 keys x 32 queries block
+__host__ __device__ inline int mpack_ntile(int N) { return (N + MPACK_T - 1) / MPACK_T; }
+__host__ __device__ inline size_t mpack_floats(int N) {
+    const size_t nt = mpack_ntile(N);
+    return nt * (nt + 1) / 2 * MPACK_T * MPACK_T;
+}
+__host__ __device__ inline int mpack_tile(int ti, int tj, int nt) { return ti * nt - ti * (ti - 1) / 2 + (tj - ti); }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 
 // ---- packed weights --------------------------------------------------------
@@ -91,6 +104,9 @@ inline PackLayout make_layout(int L, int in_dim) {
 // ---- launchers --------------------------------------------------------------
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
                          float *M, hipStream_t s);
+// Mp: [B][mpack_floats(N)]
+hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
+                                float *Mp, hipStream_t s);
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
                              const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
@@ -100,8 +116,10 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 // Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
 int attention_nsplit(int B, int N);
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element).
+// M: dense [B][N][N], or symmetric-packed [B][mpack_floats(N)] when m_packed.
 hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
-                            int B, int N, int Npad, int nsplit, float *opart, float *ml, hipStream_t s);
+                            bool m_packed, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+                            hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
 hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
                             _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s);

@@ -20,7 +20,7 @@ constexpr int SQ = 64;  // rows per workgroup
 
 __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict__ src,
                                                         const float *__restrict__ conf, int N,
-                                                        float R, float *__restrict__ lm) {
+                                                        float R2, float *__restrict__ lm) {
     __shared__ f32x4 tile[256];
     __shared__ int part[4][SQ];
     const int b = blockIdx.y, tid = threadIdx.x, q = tid >> 6, il = tid & 63;
@@ -42,14 +42,16 @@ __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict_
         tile[tid] = (j < N) ? f32x4{src[3 * j], src[3 * j + 1], src[3 * j + 2], conf[j]}
                             : f32x4{0.0f, 0.0f, 0.0f, -INFINITY};
         __syncthreads();
-#pragma unroll 4
+        // violation: c_i < c_j and !(|s_i - s_j| >= R), the latter as !(x >= R2) on the
+        // squared norm (sqrt_ge_threshold: exact, no sqrtf, branch-free)
+        bool bad = false;
+#pragma unroll 8
         for (int jj = q * 64; jj < q * 64 + 64; ++jj) {
             const f32x4 pj = tile[jj];
-            if (ci < pj[3]) {  // relation false unless the pair is out of radius
-                const float d = pdist3(xi, yi, zi, pj[0], pj[1], pj[2]);
-                if (!(d >= R)) ok = false;
-            }
+            const float x = sqdist3(xi, yi, zi, pj[0], pj[1], pj[2]);
+            bad |= (ci < pj[3]) & !(x >= R2);
         }
+        if (bad) ok = false;
     }
     part[q][il] = ok;
     __syncthreads();
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict_
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s) {
     hipLaunchKernelGGL(local_max_kernel, dim3((N + SQ - 1) / SQ, B), dim3(256), 0, s, src, conf, N,
-                       radius, lm);
+                       sqrt_ge_threshold(radius), lm);
     return hipGetLastError();
 }
 

@@ -245,3 +245,62 @@ def test_full_size_registration_properties(preset, gpu_device):
         assert re < 1.0 and te < 0.2 * p["inlier_threshold"] * 10, (re, te)
         assert labels[i].sum() >= 0.9 * b["gt_labels"][i].sum()
         assert set(np.unique(labels[i])) <= {0.0, 1.0}
+
+
+@pytest.mark.parametrize("scale,sigma", [(1e-3, 1e-4), (3.0, 0.1), (60.0, 1.2), (5e3, 37.0)])
+def test_compat_bit_exact_random_scales(scale, sigma, gpu_device):
+    """a1 against the oracle's bit-exact C restatement (oracle/exact.c) on random
+    clouds over six decades of coordinate scale, duplicate points included:
+    the kernel's fast sqrt/division path and its library fallback must both
+    reproduce the reference's correctly rounded sqrtf and '/'."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    rng = np.random.RandomState(int(scale * 7) % 1000)
+    B, N = 3, 517
+    src = (rng.rand(B, N, 3) * scale).astype(np.float32)
+    tgt = (src + rng.randn(B, N, 3).astype(np.float32) * np.float32(sigma)).astype(np.float32)
+    src[:, 5] = src[:, 9]  # duplicate points: squared distance exactly 0
+    tgt[:, 7] = tgt[:, 8]
+    src[:, 11] = src[:, 12] + np.float32(1e-20)  # a tiny positive squared distance -> library path
+    sd = torch.tensor([sigma], dtype=torch.float32, device=gpu_device)
+    M = kernels.compat(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(M[b], O.compat(src[b], tgt[b], float(np.float32(sigma)))), b
+
+
+@pytest.mark.parametrize("radius", [0.05, 0.1, 0.6])
+def test_local_max_bit_exact_random(radius, gpu_device):
+    """a5's NMS (squared-distance threshold form) against the oracle's sqrtf form."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    rng = np.random.RandomState(3)
+    B, N = 2, 1500
+    src = (rng.rand(B, N, 3) * 1.5).astype(np.float32)
+    conf = rng.randn(B, N).astype(np.float32)
+    conf[:, 10:20] = conf[:, 0:1]  # ties
+    seeds, lm = kernels.pick_seeds(_t(src, gpu_device), _t(conf, gpu_device), radius, 150)
+    lm = lm.cpu().numpy()
+    for b in range(B):
+        assert np.array_equal(lm[b], O.local_max(src[b], conf[b], radius)), b
+
+
+@pytest.mark.parametrize("N", [300, 2000, 5000])
+def test_seed_knn_random(N, gpu_device):
+    """a6 (split-fp16 distances + register radix select) against the oracle's
+    fp32 restatement, up to near-ties (assert_knn_equivalent); duplicate rows
+    make exact distance ties that must resolve by ascending index."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    rng = np.random.RandomState(N)
+    f = rng.randn(1, N, 128).astype(np.float32)
+    f[0, 50:60] = f[0, 40]  # exact ties
+    f /= np.linalg.norm(f, axis=-1, keepdims=True)
+    S = N // 10
+    seeds = rng.choice(N, S, replace=False).astype(np.int32)
+    seeds[0] = 40
+    k = 40
+    knn = kernels.seed_knn(_t(f, gpu_device), _t(seeds[None], gpu_device, torch.int32), k)[0].cpu().numpy()
+    ref = O.knn_seed_rows(f[0], seeds.astype(np.int64), k)
+    assert_knn_equivalent(knn, ref, f[0], seeds)
+    # the tie group of seed 40 (rows 40, 50..59 identical): ascending index after the dropped first
+    assert list(knn[0][:10]) == list(ref[0][:10])

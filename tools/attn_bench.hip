@@ -48,7 +48,8 @@ void run_variant(const float *q, const float *k, const float *v, const float *M,
 }
 
 static _Float16 *g_qs = nullptr;  // split layouts (allocated in main)
-template <int NW, bool XCD>
+static float *g_mp = nullptr;     // symmetric-packed M (allocated in main)
+template <int NW, bool XCD, bool PACKED = false>
 void run_h3(const float *q, const float *k, const float *v, const float *M, int B, int N, float *op,
             float *ml, float *out, hipStream_t s) {
     AttnGridH3 g = attention_h3_grid<NW>(B, N, 1024);
@@ -61,8 +62,8 @@ void run_h3(const float *q, const float *k, const float *v, const float *M, int 
         split_done = true;
     }
     const int G = g.B * g.nqb * g.nsplit;
-    hipLaunchKernelGGL((attention_h3_kernel<NW, XCD>), dim3(G), dim3(NW * 64), attention_h3_lds_bytes<NW>(), s,
-                       g_qs, g_qs + per, g_qs + 2 * per, M, g, op, ml);
+    hipLaunchKernelGGL((attention_h3_kernel<NW, XCD, PACKED>), dim3(G), dim3(NW * 64), attention_h3_lds_bytes<NW>(), s,
+                       g_qs, g_qs + per, g_qs + 2 * per, PACKED ? g_mp : M, g, op, ml);
     CK(hipGetLastError());
     if (out) hipLaunchKernelGGL(combine_k, dim3(N, B), dim3(CH), 0, s, op, ml, N, g.Npad, g.nsplit, out);
 }
@@ -74,6 +75,8 @@ int main(int argc, char **argv) {
     std::vector<Variant> V = {
         {"nw4 kt32 exp2 xcd1     ", run_variant<4, 32, true, true>},
         {"h3 nw4 xcd1            ", run_h3<4, true>},
+        {"h3 nw4 xcd1 packedM    ", run_h3<4, true, true>},
+        {"h3 nw4 xcd0 packedM    ", run_h3<4, false, true>},
     };
     size_t nq = (size_t)B * Npad * CH;
     std::vector<float> hq(nq * 3, 0.f), hp((size_t)B * N * 6);
@@ -99,6 +102,8 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(dp, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dsd, &sd, 4, hipMemcpyHostToDevice));
     CK(launch_compat(dp, dp + (size_t)B * N * 3, B, N, dsd, dM, 0));
+    CK(hipMalloc(&g_mp, (size_t)B * mpack_floats(N) * 4));
+    CK(launch_compat_packed(dp, dp + (size_t)B * N * 3, B, N, dsd, g_mp, 0));
     const float *Q = dq, *K = dq + nq, *Vv = dq + 2 * nq;
     // correctness vs variant 0
     V[0].launch(Q, K, Vv, dM, B, N, dop, dml, dref, 0);
