@@ -98,6 +98,22 @@ class EventPool:
             self.hip.hipEventDestroy(self.ct.c_void_p(self.ev[i]))
 
 
+def profiled(kernel, grid_threads):
+    """The committed rocprofv3 numbers (profiles/traffic_current.json, written by
+    tools/summarize_profile.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this bench) for one kernel at one launch shape: HBM bytes per dispatch
+    (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 read correction) and the profiled
+    average duration.  None when no profile of that shape is committed."""
+    path = os.path.join(ROOT, "profiles", "traffic_current.json")
+    try:
+        with open(path) as f:
+            prof = json.load(f)
+        ent = prof["kernels"][kernel][str(grid_threads)]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {"tag": prof["tag"], "hbm_bytes": ent.get("hbm_bytes"), "avg_ms": ent["avg_us"] / 1e3}
+
+
 def path_bytes(N, S, k, C=128):
     """algorithmic HBM bytes of compat + power-iteration path for one pair."""
     return 24.0 * N + 4.0 * N * N + S * k * (C + 6) * 4.0 + 4.0 * S * k
@@ -225,9 +241,15 @@ def main():
         att_ms = sum(att_times) / len(att_times)
         flops = P * 4.0 * N * N * 128
         achieved = flops / (att_ms * 1e-3) / 1e12
+        npad, nsplit = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(L.pdsc_attention_layout(P, N, ctypes.byref(npad), ctypes.byref(nsplit)), "attention_layout")
+        att_prof = profiled("attention_h3_kernel<4>", P * (npad.value // 128) * nsplit.value * 256)
         roofline = {"kernel": "attention_h3_kernel<4,xcd>", "bound": "mfma",
                     "achieved": round(achieved, 3), "peak": round(PEAK_H3_TFLOPS, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / PEAK_H3_TFLOPS, 4), "traffic": None,
+                    "frac": round(achieved / PEAK_H3_TFLOPS, 4),
+                    "traffic": att_prof and att_prof["hbm_bytes"],
+                    "traffic_unit": "HBM bytes per launch (rocprofv3 2*FETCH_SIZE+WRITE_SIZE)",
+                    "profile": att_prof,
                     "peak_note": "fp16 MFMA 2500 TFLOP/s / 3 products per fp32 product; "
                                  "exact-fp32 MFMA peak is 157.3",
                     "fp16_mfma_util": round(3 * achieved / PEAK_F16_MFMA_TFLOPS, 4),
@@ -243,9 +265,12 @@ def main():
         c_ms = event_time(comp, args.kernel_iters, stream)
         cbytes = P * (4.0 * N * N + 24.0 * N)
         cach = cbytes / (c_ms * 1e-3) / 1e9
+        ntile = (N + 63) // 64
+        c_prof = profiled("compat_kernel", ntile * (ntile + 1) // 2 * P * 256)
         roofline_hbm = {"kernel": "compat_kernel", "bound": "hbm", "achieved": round(cach, 1),
                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(cach / PEAK_HBM_GBS, 4),
-                        "traffic": None, "launch_ms": round(c_ms, 4), "bytes_per_launch": cbytes}
+                        "traffic": c_prof and c_prof["hbm_bytes"], "profile": c_prof,
+                        "launch_ms": round(c_ms, 4), "bytes_per_launch": cbytes}
 
         stage_ms, _ = sev.stage_means()
         stages = {k: round(v, 4) for k, v in stage_ms.items()}

@@ -1,24 +1,51 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile.sh run into profiles/<tag>_summary.md (+ copies of
-the rocprofv3 kernel_stats.csv).  FETCH_SIZE / WRITE_SIZE are rocprofv3's KB
-per dispatch; per MI355X_MICROARCH.md §HBM, FETCH_SIZE under-reports wide
-coalesced streaming reads by 2x on gfx950, so `hbm_read_corrected` = 2 x
-FETCH_SIZE is an upper-bound correction (exact only for 16-B/lane streams).
+"""Summarise a tools/profile.sh run into profiles/<tag>_summary.md, the raw
+rocprofv3 kernel_stats.csv, and profiles/<tag>_traffic.json.
+
+A bench run launches the same kernel at several shapes (the batched headline
+forward, the N=5000 path forward, single-pair forwards), so every row is keyed
+by (kernel, grid size): the per-grid average is what bench.py's HIP-event
+launch time must agree with.
+
+HBM counters (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KB
+(1024 B) per dispatch from separate --pmc passes.  On gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced streaming read, so `hbm_bytes` =
+2 x FETCH_SIZE + WRITE_SIZE (the read correction is exact for 16-B/lane
+streams and an upper bound for narrower reads).
 
 Usage: python tools/summarize_profile.py <tag> [gpurun_out/prof_<tag>]
 """
 import csv
+import glob
+import json
 import os
+import re
 import shutil
+import subprocess
 import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def short(name):
-    n = name.split("(")[0]
-    return n.replace("pdsc::", "")
+def demangle(names):
+    names = sorted(set(names))
+    try:
+        out = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True,
+                             check=True).stdout.splitlines()
+    except (OSError, subprocess.CalledProcessError):
+        out = names
+    res = {}
+    for n, d in zip(names, out):
+        if d.startswith("_Z"):  # binutils' c++filt predates _Float16 (DF16_) mangling
+            m = re.match(r"_ZN4pdsc(\d+)", d)
+            if m:
+                ln = int(m.group(1))
+                base = d[m.end():m.end() + ln]
+                targs = re.match(r"IL[ib](\d+)E", d[m.end() + ln:])
+                d = base + (f"<{targs.group(1)}>" if targs else "")
+        res[n] = d.split("(")[0].replace("pdsc::", "").replace("void ", "")
+    return res
 
 
 def main(tag, src=None):
@@ -27,37 +54,55 @@ def main(tag, src=None):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
-    rows = list(csv.DictReader(open(stats)))
-    pmc = defaultdict(lambda: defaultdict(list))
-    import glob
+    trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    pmc_rows = []
     for p in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
-        for r in csv.DictReader(open(p)):
-            pmc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        pmc_rows += list(csv.DictReader(open(p)))
+    dm = demangle([r["Kernel_Name"] for r in trace] + [r["Kernel_Name"] for r in pmc_rows])
+
+    dur = defaultdict(list)
+    for r in trace:
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        dur[(dm[r["Kernel_Name"]], g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    pmc = defaultdict(lambda: defaultdict(list))
+    for r in pmc_rows:
+        pmc[(dm[r["Kernel_Name"]], int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
     extra = sorted({c for k in pmc.values() for c in k} - {"FETCH_SIZE", "WRITE_SIZE"})
+
+    def mean(v):
+        return sum(v) / len(v) if v else float("nan")
+
+    keys = sorted(dur, key=lambda k: -sum(dur[k]))
     lines = [f"# rocprofv3 summary `{tag}`", "",
-             "Kernel-trace stats (`rocprofv3 --kernel-trace --stats`) and per-dispatch HBM counters "
-             "from separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes of the same command "
-             "(see tools/profile.sh).  KB = rocprofv3 units (1024 B).", "",
-             "| kernel | calls | avg us | total ms | % | FETCH_SIZE KB/dispatch | 2x FETCH (corr.) MB | WRITE_SIZE KB/dispatch |",
+             "`rocprofv3 --kernel-trace --stats` of `bench.py` (tools/profile.sh) plus separate `--pmc` "
+             "passes of the same command.  Rows are (kernel, grid threads): one bench run launches each "
+             "kernel at the headline shape and at the N=5000 path / single-pair shapes.  FETCH/WRITE in "
+             "KB (1024 B) per dispatch; `HBM MB` = (2 x FETCH + WRITE) x 1024 B (gfx950 FETCH_SIZE "
+             "under-counts wide reads by 2x, MI355X_MICROARCH.md §HBM).", "",
+             "| kernel | grid threads | calls | avg us | total ms | FETCH KB | WRITE KB | HBM MB/dispatch |",
              "|---|---|---|---|---|---|---|---|"]
-    for r in rows:
-        k = short(r["Name"])
-        f = pmc[k]["FETCH_SIZE"]
-        w = pmc[k]["WRITE_SIZE"]
-        fa = sum(f) / len(f) if f else float("nan")
-        wa = sum(w) / len(w) if w else float("nan")
-        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} | "
-                     f"{float(r['TotalDurationNs']) / 1e6:.3f} | {float(r['Percentage']):.2f} | "
-                     f"{fa:.0f} | {2 * fa * 1024 / 1e6:.1f} | {wa:.0f} |")
+    traffic = {}
+    for k in keys:
+        name, g = k
+        f, w = mean(pmc[k]["FETCH_SIZE"]), mean(pmc[k]["WRITE_SIZE"])
+        hbm = (2 * f + w) * 1024
+        lines.append(f"| {name} | {g} | {len(dur[k])} | {mean(dur[k]):.2f} | {sum(dur[k]) / 1e3:.3f} | "
+                     f"{f:.0f} | {w:.0f} | {hbm / 1e6:.1f} |")
+        traffic.setdefault(name, {})[str(g)] = {
+            "calls": len(dur[k]), "avg_us": round(mean(dur[k]), 3),
+            "fetch_kb": None if f != f else round(f, 1), "write_kb": None if w != w else round(w, 1),
+            "hbm_bytes": None if hbm != hbm else round(hbm)}
     if extra:
         lines += ["", "Other counters (mean per dispatch):", "",
-                  "| kernel | " + " | ".join(extra) + " |", "|---|" + "---|" * len(extra)]
-        for r in rows:
-            k = short(r["Name"])
-            vals = [sum(pmc[k][c]) / len(pmc[k][c]) if pmc[k][c] else float("nan") for c in extra]
-            lines.append(f"| {k} | " + " | ".join(f"{v:.4g}" for v in vals) + " |")
-    out = os.path.join(dst, f"{tag}_summary.md")
-    open(out, "w").write("\n".join(lines) + "\n")
+                  "| kernel | grid | " + " | ".join(extra) + " |", "|---|---|" + "---|" * len(extra)]
+        for k in keys:
+            vals = [mean(pmc[k][c]) for c in extra]
+            lines.append(f"| {k[0]} | {k[1]} | " + " | ".join(f"{v:.4g}" for v in vals) + " |")
+            for c, v in zip(extra, vals):
+                if v == v:
+                    traffic[k[0]][str(k[1])][c] = v
+    open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
 
 
