@@ -3,8 +3,8 @@
 //
 //   knn_dist     a6  seed rows of 2 - 2 F F^T (3-product fp16 MFMA), [B][S][N]
 //   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed,
-//                    row in registers): 8-bit radix select from the highest
-//                    differing bit + ordered ballot compaction
+//                    row in registers): lane-minimum threshold + compaction +
+//                    (key, index) ranking; radix-select fallback
 //   nsm_local    a7  gather k neighbours, k x k feature*spatial consistency T
 //   nsm_iter     a8  all num_iterations power iterates + per-iterate allclose flags
 //   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
@@ -22,20 +22,31 @@ namespace pdsc {
 // on the fp16 matrix cores with the 3-product split of attention_h3.hpp
 // (|error| <= 2^-21 on a distance in [0, 4], i.e. fp32-equivalent): ns is the
 // split copy of normed, [B][N][2][128] fp16 in qk_pos order (pw_last writes it).
-// A wave = 32 seeds (lane <-> seed fragment, held in registers) x KPW tiles
-// of 32 keys (lane <-> key: the accumulator register r is seed row
-// acc_row(r, h), so each store instruction writes 128 contiguous bytes).
-constexpr int KNN_KPW = 2;
+// A workgroup = 4 waves = 4 tiles of 32 seeds (lane <-> seed fragment, held in
+// registers) sweeping the same KNN_KPW tiles of 32 keys, so each key tile is
+// fetched from L2 once per workgroup and served to the other waves from L1;
+// the keys are the MFMA's row operand, so each lane ends up with 4 runs of 4
+// consecutive keys of its seed's row (16-B stores).  Workgroups are laid out
+// pair-major and remapped so that a pair's workgroups share one XCD (and its
+// L2 holds that pair's split features).
+constexpr int KNN_KPW = 8;
 
 __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
-                                                       const int *__restrict__ seeds, int N, int S,
-                                                       float *__restrict__ dist) {
-    const int b = blockIdx.z, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+                                                       const int *__restrict__ seeds, int N, int S, int nkb,
+                                                       int nsg, float *__restrict__ dist) {
+    const int G = gridDim.x;
+    int lid = blockIdx.x;
+    const int full = G & ~7;
+    if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
+    const int kb = lid % nkb, sg = (lid / nkb) % nsg, b = lid / nkb / nsg;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, l32 = lane & 31;
-    const int s0 = blockIdx.y * 32;
+    const int s0 = (sg * 4 + wave) * 32;
+    if (s0 >= S) return;  // wave-uniform; no barriers below
     const _Float16 *F = ns + (size_t)b * N * 2 * CH;
     const int sidx = s0 + l32;
     const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
+    const bool vec = (N & 3) == 0;  // dist rows 16-B aligned
     f16x8 ah[8], al[8];
     {
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
@@ -46,22 +57,34 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
         }
     }
     for (int kt = 0; kt < KNN_KPW; ++kt) {
-        const int j0 = ((blockIdx.x * 4 + wave) * KNN_KPW + kt) * 32;
+        const int j0 = (kb * KNN_KPW + kt) * 32;
         if (j0 >= N) break;  // wave-uniform
         const int j = j0 + l32;
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(j, N - 1) * 2 * CH);
         f32x16 acc = zero16();
+        // keys as the A operand: accumulator rows = keys, lane l32 = seed s0 + l32,
+        // registers 4q..4q+3 = keys j0 + 8q + 4h + 0..3 -> one 16-B store each
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const f16x8 bh = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * i + h));
             const f16x8 bl = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * i + h));
-            acc = mfma_h3(ah[i], al[i], bh, bl, acc);
+            acc = mfma_h3(bh, bl, ah[i], al[i], acc);
         }
-        if (j < N) {
+        if (sidx < S) {
+            float *drow = dist + ((size_t)b * S + sidx) * N;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int s = s0 + acc_row(r, h);
-                if (s < S) dist[((size_t)b * S + s) * N + j] = 2.0f - 2.0f * acc[r];
+            for (int q = 0; q < 4; ++q) {
+                const int jq = j0 + 8 * q + 4 * h;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = 2.0f - 2.0f * acc[4 * q + e];
+                if (vec && jq + 3 < N) {
+                    *reinterpret_cast<f32x4 *>(drow + jq) = v;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (jq + e < N) drow[jq + e] = v[e];
+                }
             }
         }
     }
@@ -69,9 +92,9 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
 
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s) {
-    const int per_block = 4 * KNN_KPW * 32;
-    hipLaunchKernelGGL(knn_dist_kernel, dim3((N + per_block - 1) / per_block, (S + 31) / 32, B), dim3(256), 0, s,
-                       ns, seeds, N, S, dist);
+    const int per_block = KNN_KPW * 32;
+    const int nkb = (N + per_block - 1) / per_block, nsg = (S + 127) / 128;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3(nkb * nsg * B), dim3(256), 0, s, ns, seeds, N, S, nkb, nsg, dist);
     return hipGetLastError();
 }
 
@@ -114,6 +137,7 @@ PDSC_DEV uint32_t fkey(float f) {
 // `need` keys in index order; the k+1 candidates are ranked by (key, index)
 // and the first is dropped positionally (models/common.py:68).
 constexpr int KNN_BINCAP = 64;
+constexpr int KNN_FASTCAP = 128;
 
 template <int R>
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int N, int S,
@@ -123,31 +147,108 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     __shared__ int cidx[4][64];
     __shared__ uint32_t bkey[4][KNN_BINCAP];
     __shared__ int bidx[4][KNN_BINCAP];
+    __shared__ uint32_t fkeyb[4][KNN_FASTCAP];
+    __shared__ int fidxb[4][KNN_FASTCAP];
     const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s = blockIdx.x * 4 + wave;
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
     const float *row = dist + ((size_t)b * S + s) * N;
-    // NI chunks of 64 keys: compile-time (fully unrolled, registers) or runtime (memory)
-    const int NI = R > 0 ? R : (N + 63) / 64;
-    uint32_t key[R > 0 ? R : 1];
-    if constexpr (R > 0) {
+    const uint32_t want = k + 1;
+    // Fast path (no atomics): tau0 = the want-th smallest of the 64 per-lane
+    // minima bounds the want-th smallest key from above (at least `want` keys are
+    // <= tau0), so every key of the answer is <= tau0.  For iid keys about
+    // 1.3 * want keys qualify; they are compacted (in any order) and ranked by
+    // (key, index).  R > 0: the row is held in registers, lane l owning keys
+    // 256 i + 4 l + e (16-B loads); R = 0: re-read from memory.  More than
+    // KNN_FASTCAP qualifying keys (heavy ties, adversarial orders) falls through
+    // to the radix select below.
+    if (want <= 64) {
+        constexpr int NR = R > 0 ? R : 1;
+        uint32_t key[NR];
+        const int NI = R > 0 ? R : (N + 63) / 64;
+        // index of this lane's i-th key
+        auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
+        if constexpr (R > 0) {
+            const bool vec = (N & 3) == 0;  // rows 16-B aligned
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-            const int j = lane + 64 * i;
-            key[i] = j < N ? fkey(row[j]) : 0xffffffffu;
+            for (int i4 = 0; i4 < R / 4; ++i4) {
+                const int j = 256 * i4 + 4 * lane;
+                if (vec && j + 3 < N) {
+                    const f32x4 v = *reinterpret_cast<const f32x4 *>(row + j);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = fkey(v[e]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = j + e < N ? fkey(row[j + e]) : 0xffffffffu;
+                }
+            }
+        }
+        auto K = [&](int i) -> uint32_t {
+            if constexpr (R > 0) {
+                return key[i];
+            } else {
+                const int j = lane + 64 * i;
+                return j < N ? fkey(row[j]) : 0xffffffffu;
+            }
+        };
+        uint32_t lmin = 0xffffffffu;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (J(i) < N) lmin = min(lmin, K(i));
+        uint32_t lrank = 0;
+        for (int t = 0; t < 64; ++t) {
+            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)lmin, t);
+            lrank += (o < lmin) || (o == lmin && t < lane);
+        }
+        const unsigned long long hitm = __ballot(lrank == want - 1);
+        const uint32_t tau0 = (uint32_t)__shfl((int)lmin, __ffsll(hitm) - 1);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int j = J(i);
+            const uint32_t u = K(i);
+            const bool q = j < N && u <= tau0;
+            const unsigned long long m = __ballot(q);
+            if (m) {
+                if (q) {
+                    const uint32_t pos = c + __popcll(m & below);
+                    if (pos < KNN_FASTCAP) {
+                        fkeyb[wave][pos] = u;
+                        fidxb[wave][pos] = j;
+                    }
+                }
+                c += __popcll(m);
+            }
+        }
+        if (c <= KNN_FASTCAP) {
+            __builtin_amdgcn_wave_barrier();
+            const int e0 = lane, e1 = lane + 64;
+            const uint32_t k0 = e0 < (int)c ? fkeyb[wave][e0] : 0xffffffffu;
+            const int i0 = e0 < (int)c ? fidxb[wave][e0] : 0x7fffffff;
+            const uint32_t k1 = e1 < (int)c ? fkeyb[wave][e1] : 0xffffffffu;
+            const int i1 = e1 < (int)c ? fidxb[wave][e1] : 0x7fffffff;
+            uint32_t r0 = 0, r1 = 0;
+            for (int m = 0; m < (int)c; ++m) {
+                const uint32_t mu = fkeyb[wave][m];
+                const int mi = fidxb[wave][m];
+                r0 += (mu < k0) || (mu == k0 && mi < i0);
+                r1 += (mu < k1) || (mu == k1 && mi < i1);
+            }
+            int *out = knn + ((size_t)b * S + s) * k;
+            if (e0 < (int)c && r0 > 0 && r0 < want) out[r0 - 1] = i0;  // drop position 0 (:68)
+            if (e1 < (int)c && r1 > 0 && r1 < want) out[r1 - 1] = i1;
+            return;
         }
     }
-    // key of chunk i for this lane (0xffffffff past the end: never selected)
+    // Radix fallback, keys re-read from memory (lane l owns keys l + 64 i, so a
+    // ballot over lanes visits keys in index order).
+    const int NI = (N + 63) / 64;
     auto K = [&](int i) -> uint32_t {
-        if constexpr (R > 0) {
-            return key[i];
-        } else {
-            const int j = lane + 64 * i;
-            return j < N ? fkey(row[j]) : 0xffffffffu;
-        }
+        const int j = lane + 64 * i;
+        return j < N ? fkey(row[j]) : 0xffffffffu;
     };
     uint32_t kmin = 0xffffffffu, kmax = 0u;
-#pragma unroll
     for (int i = 0; i < NI; ++i) {
         if (lane + 64 * i < N) {
             const uint32_t u = K(i);
@@ -161,7 +262,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
     }
     uint32_t *hb = hist[wave];
-    const uint32_t want = k + 1;
     uint32_t need = want, prefix = kmin, mask = 0xffffffffu, bin_cnt = want;
     bool small_bin = false;  // the bin holding the (k+1)-th key has <= KNN_BINCAP keys: rank them directly
     if (kmin != kmax) {
@@ -174,7 +274,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
 #pragma unroll
             for (int e = 0; e < 4; ++e) hb[lane + 64 * e] = 0;
             __builtin_amdgcn_wave_barrier();
-#pragma unroll
             for (int i = 0; i < NI; ++i) {
                 const uint32_t u = K(i);
                 if (lane + 64 * i < N && (u & mask) == prefix) atomicAdd(&hb[(u >> lo) & dm], 1u);
@@ -227,7 +326,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     const uint32_t nless = want - need;
     const unsigned long long below = (1ull << lane) - 1ull;
     uint32_t pl = 0, pe = 0;
-#pragma unroll
     for (int i = 0; i < NI; ++i) {
         const int j = lane + 64 * i;
         const uint32_t u = K(i);

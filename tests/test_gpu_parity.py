@@ -304,3 +304,28 @@ def test_seed_knn_random(N, gpu_device):
     assert_knn_equivalent(knn, ref, f[0], seeds)
     # the tie group of seed 40 (rows 40, 50..59 identical): ascending index after the dropped first
     assert list(knn[0][:10]) == list(ref[0][:10])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,dups", [(40, 0), (63, 0), (63, 300), (40, 300), (8, 2)])
+def test_seed_knn_select_paths(k, dups, gpu_device):
+    """knn_select's lane-minimum threshold fast path (want = k+1 <= 64, <= 128
+    qualifying keys) and its radix fallback (`dups` copies of a seed's
+    row giving > 128 keys tied at the threshold) pick the same (key, index)-ordered
+    neighbours as the oracle."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    N = 3000
+    rng = np.random.RandomState(7 + k + dups)
+    f = rng.randn(1, N, 128).astype(np.float32)
+    if dups:
+        f[0, 1000:1000 + dups] = f[0, 5]
+    f /= np.linalg.norm(f, axis=-1, keepdims=True)
+    seeds = rng.choice(N, 200, replace=False).astype(np.int32)
+    seeds[0] = 5
+    seeds[1] = 1000
+    knn = kernels.seed_knn(_t(f, gpu_device), _t(seeds[None], gpu_device, torch.int32), k)[0].cpu().numpy()
+    ref = O.knn_seed_rows(f[0], seeds.astype(np.int64), k)
+    assert_knn_equivalent(knn, ref, f[0], seeds)
+    if dups:
+        assert list(knn[0]) == list(ref[0])  # the tie group resolves by ascending index
