@@ -180,6 +180,30 @@ int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *
 int32_t pdsc_post_refine(float *trans, const float *src, const float *tgt, int32_t B, int32_t N,
                          float thr, pdsc_stream_t stream);
 
+/* ---------------------------------- f1 correspondence construction --------
+ * Mutual nearest neighbours in descriptor space and the network inputs built
+ * from them: replaces datasets/ThreeDMatch.py:277-308 (3DMatch / 3DLoMatch
+ * test sets), datasets/KITTI.py:85-99 and demo_registration.py:101-108.
+ *   distance = sqrt(2 - 2 src_desc tgt_desc^T + 1e-6) in fp32, never stored;
+ *   nn_src[i] = argmin_j, nn_tgt[j] = argmin_i (first index on ties, like
+ *   numpy.argmin).  src_desc [Ns,D], tgt_desc [Nt,D], 1 <= D <= 64.
+ * Workspace: 8 (Ns + Nt) bytes (64-bit key/index words).                    */
+size_t pdsc_mutual_nn_workspace_bytes(int32_t Ns, int32_t Nt);
+int32_t pdsc_mutual_nn(const float *src_desc, const float *tgt_desc, int32_t Ns, int32_t Nt, int32_t D,
+                       int32_t *nn_src, int32_t *nn_tgt, void *workspace, size_t workspace_bytes,
+                       pdsc_stream_t stream);
+/* The correspondence set (mutual != 0: i with nn_tgt[nn_src[i]] == i, in
+ * ascending i; else every i) and the forward's inputs: corr [Ns,2] int32
+ * (first *count rows valid), src_keypts / tgt_keypts [Ns,3], corr_pos [Ns,6]
+ * = [src, tgt] - their mean (numpy's sequential fp32 column mean), and, when
+ * gt_trans (a device double[16], row-major 4x4) is non-NULL, labels [Ns] =
+ * |R src + t - tgt| < inlier_threshold in fp64.  count: a device int32.     */
+int32_t pdsc_build_correspondences(const float *src_desc, const float *tgt_desc, const float *src_xyz,
+                                   const float *tgt_xyz, int32_t Ns, int32_t Nt, int32_t D, int32_t mutual,
+                                   const double *gt_trans, double inlier_threshold, int32_t *corr,
+                                   int32_t *count, float *corr_pos, float *src_keypts, float *tgt_keypts,
+                                   float *labels, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
+
 /* ----------------------------------------------- full testing forward ------
  * PointDSC.forward(data) with 'testing' in data (models/PointDSC.py:128-197)
  * for B independent pairs: compat -> encoder -> classifier -> seeds -> kNN ->

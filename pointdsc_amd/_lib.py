@@ -61,6 +61,10 @@ _PROTOS = {
     "pdsc_seed_hypotheses": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_float,
                                        vp, vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_post_refine": (c_int32, [vp, vp, vp, c_int32, c_int32, c_float, vp]),
+    "pdsc_mutual_nn_workspace_bytes": (c_size_t, [c_int32, c_int32]),
+    "pdsc_mutual_nn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, vp, vp, vp, c_size_t, vp]),
+    "pdsc_build_correspondences": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, vp, c_double,
+                                             vp, vp, vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
                                        c_size_t, vp]),

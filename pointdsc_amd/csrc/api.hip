@@ -198,6 +198,19 @@ int need_ws(size_t have, size_t need) {
         if (r_ != PDSC_OK) return r_; \
     } while (0)
 
+namespace {
+int32_t check_nn_args(const float *a, const float *b, int32_t Ns, int32_t Nt, int32_t D, void *ws, size_t ws_bytes) {
+    if (!a || !b || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (Ns < 1 || Nt < 1 || D < 1 || D > 64) return fail(PDSC_ERR_ARG, "Ns=%d Nt=%d D=%d (1 <= D <= 64)", Ns, Nt, D);
+    return need_ws(ws_bytes, pdsc_mutual_nn_workspace_bytes(Ns, Nt));
+}
+
+__global__ void unpack_nn_kernel(const unsigned long long *key, int n, int32_t *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (int32_t)(uint32_t)key[i];
+}
+}  // namespace
+
 extern "C" {
 
 const char *pdsc_version(void) { return "pdsc 0.1.0 gfx950"; }
@@ -535,6 +548,45 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     if (conf_out) HIPCHK(hipMemcpyAsync(conf_out, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
     if (seeds_out)
         HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    return PDSC_OK;
+}
+
+
+// ------------------------------------------------- f1 correspondence construction
+size_t pdsc_mutual_nn_workspace_bytes(int32_t Ns, int32_t Nt) {
+    return align_bytes((size_t)Ns * 8) + align_bytes((size_t)Nt * 8);
+}
+
+
+int32_t pdsc_mutual_nn(const float *src_desc, const float *tgt_desc, int32_t Ns, int32_t Nt, int32_t D,
+                       int32_t *nn_src, int32_t *nn_tgt, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_nn_args(src_desc, tgt_desc, Ns, Nt, D, ws, ws_bytes));
+    if (!nn_src || !nn_tgt) return fail(PDSC_ERR_ARG, "null pointer");
+    hipStream_t s = S_(stream);
+    Carve c(ws);
+    unsigned long long *rk = c.take<unsigned long long>(Ns), *ck = c.take<unsigned long long>(Nt);
+    HIPCHK(launch_nn_argmin(src_desc, tgt_desc, Ns, Nt, D, rk, ck, s));
+    hipLaunchKernelGGL(unpack_nn_kernel, dim3((Ns + 255) / 256), dim3(256), 0, s, rk, Ns, nn_src);
+    hipLaunchKernelGGL(unpack_nn_kernel, dim3((Nt + 255) / 256), dim3(256), 0, s, ck, Nt, nn_tgt);
+    HIPCHK(hipGetLastError());
+    return PDSC_OK;
+}
+
+int32_t pdsc_build_correspondences(const float *src_desc, const float *tgt_desc, const float *src_xyz,
+                                   const float *tgt_xyz, int32_t Ns, int32_t Nt, int32_t D, int32_t mutual,
+                                   const double *gt_trans, double inlier_threshold, int32_t *corr,
+                                   int32_t *count, float *corr_pos, float *src_keypts, float *tgt_keypts,
+                                   float *labels, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_nn_args(src_desc, tgt_desc, Ns, Nt, D, ws, ws_bytes));
+    if (!src_xyz || !tgt_xyz || !corr || !count || !corr_pos || !src_keypts || !tgt_keypts)
+        return fail(PDSC_ERR_ARG, "null pointer");
+    if (gt_trans && !labels) return fail(PDSC_ERR_ARG, "gt_trans given without labels");
+    hipStream_t s = S_(stream);
+    Carve c(ws);
+    unsigned long long *rk = c.take<unsigned long long>(Ns), *ck = c.take<unsigned long long>(Nt);
+    HIPCHK(launch_nn_argmin(src_desc, tgt_desc, Ns, Nt, D, rk, ck, s));
+    HIPCHK(launch_corr_build(rk, ck, src_xyz, tgt_xyz, Ns, mutual ? 1 : 0, gt_trans, inlier_threshold, corr, count,
+                             corr_pos, src_keypts, tgt_keypts, gt_trans ? labels : nullptr, s));
     return PDSC_OK;
 }
 

@@ -22,31 +22,20 @@ namespace pdsc {
 // on the fp16 matrix cores with the 3-product split of attention_h3.hpp
 // (|error| <= 2^-21 on a distance in [0, 4], i.e. fp32-equivalent): ns is the
 // split copy of normed, [B][N][2][128] fp16 in qk_pos order (pw_last writes it).
-// A workgroup = 4 waves = 4 tiles of 32 seeds (lane <-> seed fragment, held in
-// registers) sweeping the same KNN_KPW tiles of 32 keys, so each key tile is
-// fetched from L2 once per workgroup and served to the other waves from L1;
-// the keys are the MFMA's row operand, so each lane ends up with 4 runs of 4
-// consecutive keys of its seed's row (16-B stores).  Workgroups are laid out
-// pair-major and remapped so that a pair's workgroups share one XCD (and its
-// L2 holds that pair's split features).
-constexpr int KNN_KPW = 8;
+// A wave = 32 seeds (lane <-> seed fragment, held in registers) x KPW tiles
+// of 32 keys (lane <-> key: the accumulator register r is seed row
+// acc_row(r, h), so each store instruction writes 128 contiguous bytes).
+constexpr int KNN_KPW = 2;
 
 __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
-                                                       const int *__restrict__ seeds, int N, int S, int nkb,
-                                                       int nsg, float *__restrict__ dist) {
-    const int G = gridDim.x;
-    int lid = blockIdx.x;
-    const int full = G & ~7;
-    if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
-    const int kb = lid % nkb, sg = (lid / nkb) % nsg, b = lid / nkb / nsg;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+                                                       const int *__restrict__ seeds, int N, int S,
+                                                       float *__restrict__ dist) {
+    const int b = blockIdx.z, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, l32 = lane & 31;
-    const int s0 = (sg * 4 + wave) * 32;
-    if (s0 >= S) return;  // wave-uniform; no barriers below
+    const int s0 = blockIdx.y * 32;
     const _Float16 *F = ns + (size_t)b * N * 2 * CH;
     const int sidx = s0 + l32;
     const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
-    const bool vec = (N & 3) == 0;  // dist rows 16-B aligned
     f16x8 ah[8], al[8];
     {
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
@@ -57,34 +46,22 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
         }
     }
     for (int kt = 0; kt < KNN_KPW; ++kt) {
-        const int j0 = (kb * KNN_KPW + kt) * 32;
+        const int j0 = ((blockIdx.x * 4 + wave) * KNN_KPW + kt) * 32;
         if (j0 >= N) break;  // wave-uniform
         const int j = j0 + l32;
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(j, N - 1) * 2 * CH);
         f32x16 acc = zero16();
-        // keys as the A operand: accumulator rows = keys, lane l32 = seed s0 + l32,
-        // registers 4q..4q+3 = keys j0 + 8q + 4h + 0..3 -> one 16-B store each
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const f16x8 bh = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * i + h));
             const f16x8 bl = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * i + h));
-            acc = mfma_h3(bh, bl, ah[i], al[i], acc);
+            acc = mfma_h3(ah[i], al[i], bh, bl, acc);
         }
-        if (sidx < S) {
-            float *drow = dist + ((size_t)b * S + sidx) * N;
+        if (j < N) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int jq = j0 + 8 * q + 4 * h;
-                f32x4 v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = 2.0f - 2.0f * acc[4 * q + e];
-                if (vec && jq + 3 < N) {
-                    *reinterpret_cast<f32x4 *>(drow + jq) = v;
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (jq + e < N) drow[jq + e] = v[e];
-                }
+            for (int r = 0; r < 16; ++r) {
+                const int s = s0 + acc_row(r, h);
+                if (s < S) dist[((size_t)b * S + s) * N + j] = 2.0f - 2.0f * acc[r];
             }
         }
     }
@@ -92,9 +69,9 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
 
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s) {
-    const int per_block = KNN_KPW * 32;
-    const int nkb = (N + per_block - 1) / per_block, nsg = (S + 127) / 128;
-    hipLaunchKernelGGL(knn_dist_kernel, dim3(nkb * nsg * B), dim3(256), 0, s, ns, seeds, N, S, nkb, nsg, dist);
+    const int per_block = 4 * KNN_KPW * 32;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3((N + per_block - 1) / per_block, (S + 31) / 32, B), dim3(256), 0, s,
+                       ns, seeds, N, S, dist);
     return hipGetLastError();
 }
 

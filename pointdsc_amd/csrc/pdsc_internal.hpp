@@ -167,4 +167,17 @@ hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, 
 hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
                         hipStream_t s);
 
+// correspondence construction (corr.hip)
+#define HIP_RET(expr)                         \
+    do {                                      \
+        hipError_t e_ = (expr);               \
+        if (e_ != hipSuccess) return e_;      \
+    } while (0)
+hipError_t launch_nn_argmin(const float *A, const float *B, int Na, int Nb, int D, unsigned long long *rowkey,
+                            unsigned long long *colkey, hipStream_t s);
+hipError_t launch_corr_build(const unsigned long long *rowkey, const unsigned long long *colkey,
+                             const float *src_xyz, const float *tgt_xyz, int Na, int mutual, const double *gt,
+                             double thr, int *corr, int *count, float *corr_pos, float *src_out, float *tgt_out,
+                             float *labels, hipStream_t s);
+
 }  // namespace pdsc

@@ -10,6 +10,6 @@ step() {  # name timeout cmd...
     local rc=$?; echo "$name rc=$rc"; tail -5 "gpurun_out/$name.log"
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step pytest_gpu 900 python -m pytest tests/test_gpu_parity.py -q -m gpu -p no:cacheprovider ${PYTEST_ARGS}
+step pytest_gpu 900 python -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 5 --warmup 2
