@@ -5,8 +5,9 @@
 //   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed,
 //                    row in registers): lane-minimum threshold + compaction +
 //                    (key, index) ranking; radix-select fallback
-//   nsm_local    a7  gather k neighbours, k x k feature*spatial consistency T
-//   nsm_iter     a8  all num_iterations power iterates + per-iterate allclose flags
+//   nsm_local    a7-a8  gather k neighbours, k x k feature*spatial consistency T
+//                    in LDS, then all num_iterations power iterates + per-iterate
+//                    allclose flags (T never written to HBM)
 //   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
 //                    is allclose (torch.allclose over the whole batch, :354)
 //   hypotheses   a9-a10  weighted Kabsch per seed (fp64 3x3 SVD on device) +
@@ -385,19 +386,57 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
 constexpr int KMAX = 64;
 constexpr int FSTR = CH + 4;
 
+// Power iteration of one seed's k x k matrix (models/PointDSC.py:347-358), one
+// wave: lane a holds row a of T in registers, v is broadcast from LDS 4 entries
+// at a time.  hist[t][a] = iterate t+1; returns bit t = allclose(v_{t+1}, v_t).
+PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T, float *vbuf, float *hb, int a) {
+    float trow[KMAX];
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c) trow[c] = (a < k && c < k) ? trow_lds[a * tstride + c] : 0.0f;
+    vbuf[a] = 1.0f;
+    float v = (a < k) ? 1.0f : 0.0f;
+    unsigned flags = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int t = 0; t < T; ++t) {
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int c = 0; c < KMAX; c += 4) {
+            const f32x4 vv = *reinterpret_cast<const f32x4 *>(&vbuf[c]);
+            acc[0] = __builtin_fmaf(trow[c], vv[0], acc[0]);
+            acc[1] = __builtin_fmaf(trow[c + 1], vv[1], acc[1]);
+            acc[2] = __builtin_fmaf(trow[c + 2], vv[2], acc[2]);
+            acc[3] = __builtin_fmaf(trow[c + 3], vv[3], acc[3]);
+        }
+        float nv = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // (T v)_a  (bmm, :352)
+        const float nrm = sqrtf(wave_sum(nv * nv));
+        nv = nv / (nrm + 1e-6f);                              // :353
+        const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
+        if (__all(close)) flags |= 1u << t;
+        if (a < k) hb[(size_t)t * k + a] = nv;
+        v = nv;
+        __builtin_amdgcn_wave_barrier();
+        vbuf[a] = nv;
+        __builtin_amdgcn_wave_barrier();
+    }
+    return flags;
+}
+
 // nsm_local: one workgroup per (seed, pair) builds the k x k matrix T of the
-// seed's neighbourhood into Tg[b][s][k][k].
+// seed's neighbourhood in LDS, then its first wave runs all T power iterates
+// (hist[b][s][t][a]) and AND-s the per-iterate allclose bits into pair_mask[b]
+// -- T never leaves the CU.
 __global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict__ normed,
                                                         const float *__restrict__ src,
                                                         const float *__restrict__ tgt,
                                                         const int *__restrict__ knn, int N, int S,
-                                                        int k, const float *__restrict__ sigma_p,
+                                                        int k, int T, const float *__restrict__ sigma_p,
                                                         const float *__restrict__ sigma_d_p,
-                                                        float *__restrict__ Tg) {
+                                                        float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
     __shared__ __attribute__((aligned(16))) float F[KMAX * FSTR];
     __shared__ float P[KMAX][6];
     __shared__ int nidx[KMAX];
-    float *Tb = Tg + ((size_t)blockIdx.y * S + blockIdx.x) * k * k;
+    __shared__ float Tl[KMAX][KMAX + 1];
+    __shared__ __attribute__((aligned(16))) float vb[KMAX];
     const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
     const float sig = sigma_p[0], sd = sigma_d_p[0];
     const float sig2 = sig * sig, sd2 = sd * sd;
@@ -463,55 +502,14 @@ __global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict_
                 const float sm = fmaxf(1.0f - (dd * dd) / sd2, 0.0f);        // :270
                 val = fm * sm;                                               // :277 (diag 0, :278)
             }
-            Tb[a * k + c] = val;
-            Tb[c * k + a] = val;
+            Tl[a][c] = val;
+            Tl[c][a] = val;
         }
     }
-}
-
-// nsm_iter: one WAVE per seed (4 seeds per workgroup) runs all T power
-// iterates (models/PointDSC.py:347-358): lane a keeps row a of T in registers,
-// v is broadcast from LDS 4 entries at a time.  hist[b][s][t][a] = iterate t+1;
-// bit t of the seed's flag word = allclose(v_{t+1}, v_t), AND-ed into pair_mask[b].
-__global__ __launch_bounds__(256) void nsm_iter_kernel(const float *__restrict__ Tg, int S, int k, int T,
-                                                       float *__restrict__ hist,
-                                                       unsigned *__restrict__ pair_mask) {
-    __shared__ __attribute__((aligned(16))) float vb[4][KMAX];
-    const int b = blockIdx.y, wave = threadIdx.x >> 6, a = threadIdx.x & 63;
-    const int s = blockIdx.x * 4 + wave;
-    if (s >= S) return;
-    float *vbuf = vb[wave];
-    vbuf[a] = 1.0f;
-    {
-        const float *Tb = Tg + ((size_t)b * S + s) * k * k;
-        float trow[KMAX];
-#pragma unroll
-        for (int c = 0; c < KMAX; ++c) trow[c] = (a < k && c < k) ? Tb[a * k + c] : 0.0f;
-        float v = (a < k) ? 1.0f : 0.0f;
-        unsigned flags = 0;
-        float *hb = hist + ((size_t)b * S + s) * T * k;
-        for (int t = 0; t < T; ++t) {
-            float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int c = 0; c < KMAX; c += 4) {
-                const f32x4 vv = *reinterpret_cast<const f32x4 *>(&vbuf[c]);
-                acc[0] = __builtin_fmaf(trow[c], vv[0], acc[0]);
-                acc[1] = __builtin_fmaf(trow[c + 1], vv[1], acc[1]);
-                acc[2] = __builtin_fmaf(trow[c + 2], vv[2], acc[2]);
-                acc[3] = __builtin_fmaf(trow[c + 3], vv[3], acc[3]);
-            }
-            float nv = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // (T v)_a  (bmm, :352)
-            const float nrm = sqrtf(wave_sum(nv * nv));
-            nv = nv / (nrm + 1e-6f);                              // :353
-            const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
-            if (__all(close)) flags |= 1u << t;
-            if (a < k) hb[(size_t)t * k + a] = nv;
-            v = nv;
-            __builtin_amdgcn_wave_barrier();
-            vbuf[a] = nv;
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (a == 0) atomicAnd(&pair_mask[b], flags);
+    __syncthreads();
+    if (tid < 64) {
+        const unsigned flags = power_iterate(&Tl[0][0], KMAX + 1, k, T, vb, hist + ((size_t)b * S + s) * T * k, tid);
+        if (tid == 0) atomicAnd(&pair_mask[b], flags);
     }
 }
 
@@ -519,9 +517,9 @@ hipError_t launch_nsm_power(const float *normed, const float *src, const float *
                             int B, int N, int S, int k, int T, const float *sigma,
                             const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
                             hipStream_t s) {
-    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), 0, s, normed, src, tgt, knn, N, S, k,
-                       sigma, sigma_d, Tg);
-    hipLaunchKernelGGL(nsm_iter_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, Tg, S, k, T, hist, pair_mask);
+    (void)Tg;  // T stays in LDS (nsm_local_kernel)
+    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), 0, s, normed, src, tgt, knn, N, S, k, T,
+                       sigma, sigma_d, hist, pair_mask);
     return hipGetLastError();
 }
 
