@@ -180,6 +180,23 @@ int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *
 int32_t pdsc_post_refine(float *trans, const float *src, const float *tgt, int32_t B, int32_t N,
                          float thr, pdsc_stream_t stream);
 
+/* ------------------------------------- f3 spectral-matching baseline -----
+ * SM of baseline_scripts/baseline_3DMatch.py:19-53 for one pair: dense
+ * M_ij = max(0, 4.5 - (|c_j - c_i|_xyz - |c_j - c_i|_xyz')^2 / 2 / sigma^2),
+ * sigma = inlier_threshold / 3, diag 0, over corr_pos [N,6]; num_iterations
+ * power iterates v <- Mv / (|Mv| + 1e-6) from v = 1; labels [N] = the
+ * int(N * top_ratio) largest entries of v (ties to the lower index); trans
+ * [4,4] = rigid_transform_3d(src, tgt, v * labels).  leading_eig [N] may be
+ * NULL.  Workspace: the dense M (4 N^2 B) + 3 vectors.                      */
+size_t pdsc_spectral_matching_workspace_bytes(int32_t N);
+int32_t pdsc_spectral_matching(const float *corr_pos, const float *src, const float *tgt, int32_t N,
+                               double inlier_threshold, double top_ratio, int32_t num_iterations, float *trans,
+                               float *labels, float *leading_eig, void *workspace, size_t workspace_bytes,
+                               pdsc_stream_t stream);
+/* One M v product of the SM power iteration (the HBM-bound kernel, exposed for
+ * measurement): y [N] = M [N,N] v [N].                                       */
+int32_t pdsc_sm_matvec(const float *M, const float *v, int32_t N, float *y, pdsc_stream_t stream);
+
 /* ---------------------------------- f1 correspondence construction --------
  * Mutual nearest neighbours in descriptor space and the network inputs built
  * from them: replaces datasets/ThreeDMatch.py:277-308 (3DMatch / 3DLoMatch

@@ -65,6 +65,10 @@ _PROTOS = {
     "pdsc_mutual_nn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, vp, vp, vp, c_size_t, vp]),
     "pdsc_build_correspondences": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, vp, c_double,
                                              vp, vp, vp, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_spectral_matching_workspace_bytes": (c_size_t, [c_int32]),
+    "pdsc_spectral_matching": (c_int32, [vp, vp, vp, c_int32, c_double, c_double, c_int32, vp, vp, vp, vp,
+                                         c_size_t, vp]),
+    "pdsc_sm_matvec": (c_int32, [vp, vp, c_int32, vp, vp]),
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
                                        c_size_t, vp]),

@@ -590,4 +590,34 @@ int32_t pdsc_build_correspondences(const float *src_desc, const float *tgt_desc,
     return PDSC_OK;
 }
 
+// ------------------------------------------------ f3 spectral-matching baseline
+size_t pdsc_spectral_matching_workspace_bytes(int32_t N) {
+    return align_bytes((size_t)N * N * sizeof(float)) + 3 * align_bytes((size_t)N * sizeof(float));
+}
+
+int32_t pdsc_spectral_matching(const float *corr_pos, const float *src, const float *tgt, int32_t N,
+                               double inlier_threshold, double top_ratio, int32_t iters, float *trans,
+                               float *labels, float *leading_eig, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    if (!corr_pos || !src || !tgt || !trans || !labels || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (N < 1 || N > 46340 || iters < 0 || !(top_ratio >= 0.0 && top_ratio <= 1.0) || !(inlier_threshold > 0.0))
+        return fail(PDSC_ERR_ARG, "N=%d iters=%d top_ratio=%g inlier_threshold=%g", N, iters, top_ratio,
+                    inlier_threshold);
+    RET_IF(need_ws(ws_bytes, pdsc_spectral_matching_workspace_bytes(N)));
+    Carve c(ws);
+    float *M = c.take<float>((size_t)N * N), *v = c.take<float>(N), *y = c.take<float>(N), *w = c.take<float>(N);
+    if (leading_eig) v = leading_eig;
+    const double sigma = inlier_threshold / 3.0;  // :34 (python float)
+    const float sig2 = (float)(sigma * sigma);    // tensor / python scalar -> fp32 divisor
+    const int S = (int)(N * top_ratio);           // int(leading_eig.shape[1] * top_ratio) (:46)
+    HIPCHK(launch_sm(corr_pos, src, tgt, N, sig2, S, iters, M, v, y, w, labels, trans, S_(stream)));
+    return PDSC_OK;
+}
+
+int32_t pdsc_sm_matvec(const float *M, const float *v, int32_t N, float *y, pdsc_stream_t stream) {
+    if (!M || !v || !y) return fail(PDSC_ERR_ARG, "null pointer");
+    if (N < 1) return fail(PDSC_ERR_ARG, "N=%d", N);
+    HIPCHK(launch_sm_matvec(M, v, N, y, S_(stream)));
+    return PDSC_OK;
+}
+
 }  // extern "C"

@@ -173,6 +173,10 @@ hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb,
         hipError_t e_ = (expr);               \
         if (e_ != hipSuccess) return e_;      \
     } while (0)
+// spectral-matching baseline (sm.hip)
+hipError_t launch_sm(const float *corr, const float *src, const float *tgt, int N, float sig2, int S, int iters,
+                     float *M, float *v, float *y, float *w, float *labels, float *trans, hipStream_t s);
+hipError_t launch_sm_matvec(const float *M, const float *v, int N, float *y, hipStream_t s);
 hipError_t launch_nn_argmin(const float *A, const float *B, int Na, int Nb, int D, unsigned long long *rowkey,
                             unsigned long long *colkey, hipStream_t s);
 hipError_t launch_corr_build(const unsigned long long *rowkey, const unsigned long long *colkey,
