@@ -76,6 +76,14 @@ int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *params_hos
  * src,tgt [B,N,3]; M [B,N,N].                                              */
 int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                         const float *sigma_d_dev, float *M, pdsc_stream_t stream);
+/* The forward's form of the same M: the upper triangle of 32 x 32 tiles, each
+ * a contiguous row-major 4 KiB block, tile (ti, tj), ti <= tj, at block index
+ * ti*nt - ti*(ti-1)/2 + (tj - ti), nt = ceil(N/32); M[i][j] for i > j is
+ * element (j%32, i%32) of tile (j/32, i/32); entries past N are 0.
+ * Mp: B * pdsc_compat_packed_floats(N) floats.                              */
+size_t pdsc_compat_packed_floats(int32_t N);
+int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
+                               const float *sigma_d_dev, float *Mp, pdsc_stream_t stream);
 
 /* -------------------------------------------------- a2-a4 encoder ----------
  * SCNonlocal encoder + F.normalize + classification MLP.

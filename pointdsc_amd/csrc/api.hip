@@ -304,6 +304,16 @@ int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N
     return PDSC_OK;
 }
 
+size_t pdsc_compat_packed_floats(int32_t N) { return N < 1 ? 0 : mpack_floats(N); }
+
+int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
+                               const float *sigma_d_dev, float *Mp, pdsc_stream_t stream) {
+    if (!src || !tgt || !sigma_d_dev || !Mp) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    HIPCHK(launch_compat_packed(src, tgt, B, N, sigma_d_dev, Mp, S_(stream)));
+    return PDSC_OK;
+}
+
 // ---------------------------------------------------------------- a2-a4
 size_t pdsc_encoder_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N) {
     Dims d;

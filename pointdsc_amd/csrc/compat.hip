@@ -40,6 +40,64 @@ PDSC_DEV float cr_div(float x, float d, float rcp) {
     return __builtin_fmaf(r, rcp, q);
 }
 
+// Per-wave LDS scratch of compat4: a queue of the elements that need the exact
+// evaluation and the wave's 4 x 64 outputs.
+struct CompatScratch {
+    float qx[256], qt[256], out[256];
+    unsigned short qs[256];
+};
+
+// M for 4 (row, column) pairs of this lane, given their squared distances.
+// M is 0 whenever |sqrt(xs) - sqrt(xt)| >= sigma_d, and
+//   |sqrt(xs) - sqrt(xt)| = |xs - xt| / (sqrt(xs) + sqrt(xt)) >= |xs - xt| / sqrt(2 (xs + xt)),
+// so (xs - xt)^2 > 2 s2 (xs + xt) (1 + 2^-10) proves M = 0 without a square
+// root (the 2^-10 slack covers the fp32 evaluation of both sides; the guard
+// xs + xt <= 2^20 s2 keeps the rounding of the correctly rounded square roots,
+// <= 2^-24 (sqrt(xs) + sqrt(xt)), below that slack).  Only the other elements
+// -- typically a fifth to a third -- are compacted into an LDS queue (ballot
+// order) and evaluated exactly, 64 per pass, so the ~40-op correctly rounded
+// sqrtf/sqrtf/'/' chain runs on full waves of useful work.
+PDSC_DEV void compat4(const float xs[4], const float xt[4], float s2, float rs2, bool s2ok, float kzero,
+                      float gmax, CompatScratch &sc, int lane, float out[4]) {
+    const unsigned long long below = (1ull << lane) - 1ull;
+    *reinterpret_cast<f32x4 *>(&sc.out[4 * lane]) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float dxt = xs[q] - xt[q], sum = xs[q] + xt[q];
+        const bool zero = (dxt * dxt > kzero * sum) && (sum <= gmax);  // NaN, xs = xt = 0 -> exact path
+        const unsigned long long m = __ballot(!zero);
+        if (!zero) {
+            const int pos = cnt + __popcll(m & below);
+            sc.qx[pos] = xs[q];
+            sc.qt[pos] = xt[q];
+            sc.qs[pos] = (unsigned short)(4 * lane + q);
+        }
+        cnt += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int c0 = 0; c0 < cnt; c0 += 64) {  // wave-uniform
+        const int e = c0 + lane;
+        const bool act = e < cnt;
+        const float x = act ? sc.qx[e] : 1.0f, t = act ? sc.qt[e] : 1.0f;
+        const bool tiny = (x != 0.0f && !(x >= 0x1p-96f)) || (t != 0.0f && !(t >= 0x1p-96f));
+        float m;
+        if (s2ok && !__any(tiny)) {
+            const float d = cr_sqrt(x) - cr_sqrt(t);
+            m = 1.0f - cr_div(d * d, s2, rs2);
+        } else {  // library sqrtf and '/' (correctly rounded in every case)
+            const float d = sqrtf(x) - sqrtf(t);
+            m = 1.0f - (d * d) / s2;
+        }
+        if (act) sc.out[sc.qs[e]] = m > 0.0f ? m : 0.0f;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const f32x4 o = *reinterpret_cast<const f32x4 *>(&sc.out[4 * lane]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = o[q];
+    __builtin_amdgcn_wave_barrier();  // the next call rewrites sc
+}
+
 __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ src,
                                                      const float *__restrict__ tgt, int N,
                                                      int ntile, const float *__restrict__ sigma_d_ptr,
@@ -152,6 +210,7 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
                                                             const float *__restrict__ sigma_d_ptr,
                                                             float *__restrict__ Mp) {
     __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
+    __shared__ CompatScratch scr[4];
     int t = blockIdx.x, ti = 0;
     while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
     const int tj = ti + t;
@@ -160,11 +219,12 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
     const float s2 = sd * sd;
     const float rs2 = 1.0f / s2;
     const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
+    const float kzero = 2.0f * s2 * (1.0f + 0x1p-10f), gmax = 0x1p20f * s2;  // compat4's zero test
     src += (size_t)b * N * 3;
     tgt += (size_t)b * N * 3;
     const int nt32 = mpack_ntile(N);
     float *Mb = Mp + (size_t)b * mpack_floats(N);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int i0 = ti * CT, j0 = tj * CT;
     for (int e = tid; e < CT * 3; e += 256) {
         const int p = e / 3, c = e % 3;
@@ -176,40 +236,35 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
     __syncthreads();
     const int cq = tid & 15, rq = tid >> 4;
     const int tc = 2 * tj + (cq >> 3);  // the 32-tile column of this thread's 4 columns
+    float cs[4][3], ct[4][3];  // this thread's 4 columns, the same for every row below
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            cs[q][k] = pts[2][cq * 4 + q][k];
+            ct[q][k] = pts[3][cq * 4 + q][k];
+        }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
         const int r = rq + 16 * rr;
         const int tr = 2 * ti + (r >> 5);
-        if (tr > tc || tr >= nt32 || tc >= nt32) continue;  // below the diagonal (diagonal block) / past N
+        // below the diagonal (diagonal block) / past N: computed (compat4 needs the
+        // whole wave) but not stored
+        const bool skip = tr > tc || tr >= nt32 || tc >= nt32;
+        if (__all(skip)) continue;  // wave-uniform
         const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
         const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
         float xs[4], xt[4], out[4];
-        bool tiny = false;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int c = cq * 4 + q;
-            xs[q] = sqdist3(six, siy, siz, pts[2][c][0], pts[2][c][1], pts[2][c][2]);
-            xt[q] = sqdist3(tix, tiy, tiz, pts[3][c][0], pts[3][c][1], pts[3][c][2]);
-            tiny |= (xs[q] != 0.0f && !(xs[q] >= 0x1p-96f)) || (xt[q] != 0.0f && !(xt[q] >= 0x1p-96f));
+            xs[q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
+            xt[q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
         }
-        if (s2ok && !__any(tiny)) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float d = cr_sqrt(xs[q]) - cr_sqrt(xt[q]);
-                const float m = 1.0f - cr_div(d * d, s2, rs2);
-                out[q] = m > 0.0f ? m : 0.0f;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float d = sqrtf(xs[q]) - sqrtf(xt[q]);
-                const float m = 1.0f - (d * d) / s2;
-                out[q] = m > 0.0f ? m : 0.0f;
-            }
-        }
+        compat4(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             if (i0 + r >= N || j0 + cq * 4 + q >= N) out[q] = 0.0f;
+        if (skip) continue;
         float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
         *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{out[0], out[1], out[2], out[3]};
     }

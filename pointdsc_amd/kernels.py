@@ -52,6 +52,27 @@ def compat(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch
     return M
 
 
+def compat_packed(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch.Tensor:
+    """The forward's symmetric-packed M (include/pdsc.h: pdsc_compat_packed_f32),
+    unpacked to dense [B,N,N] on the device for inspection."""
+    src, tgt = _dev(src, "src"), _dev(tgt, "tgt")
+    sigma_d = _dev(sigma_d.reshape(-1), "sigma_d")
+    B, N, _ = src.shape
+    L = _lib.load()
+    nf = L.pdsc_compat_packed_floats(N)
+    Mp = torch.empty((B, nf), dtype=torch.float32, device=src.device)
+    check(L.pdsc_compat_packed_f32(_p(src), _p(tgt), B, N, _p(sigma_d), _p(Mp), _stream(src.device)),
+          "pdsc_compat_packed_f32")
+    T = 32
+    nt = (N + T - 1) // T
+    ti, tj = torch.triu_indices(nt, nt)
+    tiles = Mp.view(B, -1, T, T)  # upper-triangle tiles in row-major (ti, tj) order
+    full = torch.zeros((B, nt, nt, T, T), dtype=torch.float32, device=src.device)
+    full[:, ti, tj] = tiles
+    full[:, tj, ti] = tiles.transpose(-1, -2)
+    return full.permute(0, 1, 3, 2, 4).reshape(B, nt * T, nt * T)[:, :N, :N].contiguous()
+
+
 # ------------------------------------------------------------------ weights
 def pack_weights(cfg: _lib.PdscConfig, named: dict) -> torch.Tensor:
     """Pack reference state-dict tensors (on device) into the kernels' blob."""

@@ -262,10 +262,14 @@ def test_compat_bit_exact_random_scales(scale, sigma, gpu_device):
     src[:, 5] = src[:, 9]  # duplicate points: squared distance exactly 0
     tgt[:, 7] = tgt[:, 8]
     src[:, 11] = src[:, 12] + np.float32(1e-20)  # a tiny positive squared distance -> library path
+    src[:, 20] = np.float32(4e3 * scale)  # far points: past compat4's sqrt-free zero test guard
     sd = torch.tensor([sigma], dtype=torch.float32, device=gpu_device)
     M = kernels.compat(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
+    Mp = kernels.compat_packed(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
     for b in range(B):
-        assert np.array_equal(M[b], O.compat(src[b], tgt[b], float(np.float32(sigma)))), b
+        ref = O.compat(src[b], tgt[b], float(np.float32(sigma)))
+        assert np.array_equal(M[b], ref), b
+        assert np.array_equal(Mp[b], ref), b
 
 
 @pytest.mark.parametrize("radius", [0.05, 0.1, 0.6])
