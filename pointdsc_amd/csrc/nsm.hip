@@ -23,22 +23,28 @@ namespace pdsc {
 // on the fp16 matrix cores with the 3-product split of attention_h3.hpp
 // (|error| <= 2^-21 on a distance in [0, 4], i.e. fp32-equivalent): ns is the
 // split copy of normed, [B][N][2][128] fp16 in qk_pos order (pw_last writes it).
-// A wave = 32 seeds (lane <-> seed fragment, held in registers) x KPW tiles
-// of 32 keys (lane <-> key: the accumulator register r is seed row
-// acc_row(r, h), so each store instruction writes 128 contiguous bytes).
-constexpr int KNN_KPW = 2;
+// A workgroup = 4 waves = 4 tiles of 32 seeds (lane <-> seed fragment, held in
+// registers for the whole launch) sweeping KNN_KPB tiles of 32 keys; each key
+// tile (32 rows x 512 B of split features, contiguous in HBM) is copied once
+// into LDS (16-B chunks XOR-swizzled by row: conflict-free fragment reads) and
+// feeds all four waves, so a wave-tile of 24 MFMAs costs ~4 KB of L2 traffic
+// instead of 24 KB.  lane <-> key in the accumulator (register r is seed row
+// acc_row(r, h)): each store instruction writes 128 contiguous bytes.
+constexpr int KNN_KPB = 5;
 
 __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
                                                        const int *__restrict__ seeds, int N, int S,
                                                        float *__restrict__ dist) {
-    const int b = blockIdx.z, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ f16x8 Bt[32 * 32];
+    const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, l32 = lane & 31;
-    const int s0 = blockIdx.y * 32;
+    const int s0 = (blockIdx.y * 4 + wave) * 32;
+    const bool active = s0 < S;  // wave-uniform; every wave joins the barriers
     const _Float16 *F = ns + (size_t)b * N * 2 * CH;
     const int sidx = s0 + l32;
-    const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
     f16x8 ah[8], al[8];
-    {
+    if (active) {
+        const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -46,17 +52,30 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
             al[j] = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * j + h));
         }
     }
-    for (int kt = 0; kt < KNN_KPW; ++kt) {
-        const int j0 = ((blockIdx.x * 4 + wave) * KNN_KPW + kt) * 32;
-        if (j0 >= N) break;  // wave-uniform
+    const int nkt = (N + 31) / 32;
+    const int t0 = blockIdx.x * KNN_KPB, t1 = min(t0 + KNN_KPB, nkt);
+    for (int t = t0; t < t1; ++t) {
+        const int j0 = t * 32;
+        f16x8 stage[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, r = e >> 5, c = e & 31;
+            stage[q] = reinterpret_cast<const f16x8 *>(F + (size_t)min(j0 + r, N - 1) * 2 * CH)[c];
+        }
+        __syncthreads();  // the previous tile's readers are done
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, r = e >> 5, c = e & 31;
+            Bt[r * 32 + (c & 16) + ((c & 15) ^ (r & 15))] = stage[q];
+        }
+        __syncthreads();
+        if (!active) continue;
         const int j = j0 + l32;
-        const char *row = reinterpret_cast<const char *>(F + (size_t)min(j, N - 1) * 2 * CH);
         f32x16 acc = zero16();
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const f16x8 bh = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * i + h));
-            const f16x8 bl = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * i + h));
-            acc = mfma_h3(ah[i], al[i], bh, bl, acc);
+            const int cc = (2 * i + h) ^ (l32 & 15);
+            acc = mfma_h3(ah[i], al[i], Bt[l32 * 32 + cc], Bt[l32 * 32 + 16 + cc], acc);
         }
         if (j < N) {
 #pragma unroll
@@ -70,8 +89,8 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
 
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s) {
-    const int per_block = 4 * KNN_KPW * 32;
-    hipLaunchKernelGGL(knn_dist_kernel, dim3((N + per_block - 1) / per_block, (S + 31) / 32, B), dim3(256), 0, s,
+    const int nkt = (N + 31) / 32;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3((nkt + KNN_KPB - 1) / KNN_KPB, (S + 127) / 128, B), dim3(256), 0, s,
                        ns, seeds, N, S, dist);
     return hipGetLastError();
 }
@@ -432,11 +451,14 @@ __global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict_
                                                         int k, int T, const float *__restrict__ sigma_p,
                                                         const float *__restrict__ sigma_d_p,
                                                         float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
-    __shared__ __attribute__((aligned(16))) float F[KMAX * FSTR];
+    // dynamic LDS sized by k (nsm_local_lds_bytes): F [kp][FSTR] then T [k][k+1]
+    extern __shared__ __attribute__((aligned(16))) float nsm_dyn[];
     __shared__ float P[KMAX][6];
     __shared__ int nidx[KMAX];
-    __shared__ float Tl[KMAX][KMAX + 1];
     __shared__ __attribute__((aligned(16))) float vb[KMAX];
+    float *F = nsm_dyn;
+    float *Tl = nsm_dyn + (size_t)((k + 1) & ~1) * FSTR;
+    const int tls = k + 1;
     const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
     const float sig = sigma_p[0], sd = sigma_d_p[0];
     const float sig2 = sig * sig, sd2 = sd * sd;
@@ -502,13 +524,13 @@ __global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict_
                 const float sm = fmaxf(1.0f - (dd * dd) / sd2, 0.0f);        // :270
                 val = fm * sm;                                               // :277 (diag 0, :278)
             }
-            Tl[a][c] = val;
-            Tl[c][a] = val;
+            Tl[a * tls + c] = val;
+            Tl[c * tls + a] = val;
         }
     }
     __syncthreads();
     if (tid < 64) {
-        const unsigned flags = power_iterate(&Tl[0][0], KMAX + 1, k, T, vb, hist + ((size_t)b * S + s) * T * k, tid);
+        const unsigned flags = power_iterate(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, tid);
         if (tid == 0) atomicAnd(&pair_mask[b], flags);
     }
 }
@@ -518,7 +540,8 @@ hipError_t launch_nsm_power(const float *normed, const float *src, const float *
                             const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
                             hipStream_t s) {
     (void)Tg;  // T stays in LDS (nsm_local_kernel)
-    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), 0, s, normed, src, tgt, knn, N, S, k, T,
+    const size_t lds = ((size_t)((k + 1) & ~1) * FSTR + (size_t)k * (k + 1)) * sizeof(float);
+    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), lds, s, normed, src, tgt, knn, N, S, k, T,
                        sigma, sigma_d, hist, pair_mask);
     return hipGetLastError();
 }
