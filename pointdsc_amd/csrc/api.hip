@@ -272,7 +272,7 @@ int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *P, float *
         return launch_pack_dense(P[wi], P[wi + 1], has_bn ? P[wi + 2] : nullptr,
                                  has_bn ? P[wi + 3] : nullptr, has_bn ? P[wi + 4] : nullptr,
                                  has_bn ? P[wi + 5] : nullptr, in, out, packed + o.w, packed + o.bias,
-                                 packed + o.alpha, packed + o.beta, s);
+                                 packed + o.alpha, packed + o.beta, packed + o.scale, s);
     };
     for (int l = 0; l < cfg->num_layers; ++l) {
         const int b = 2 + 26 * l;

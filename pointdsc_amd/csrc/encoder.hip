@@ -10,9 +10,10 @@
 // Kernels per forward: pw_first (layer0 + PointCN_0 + QKV_0), then per layer
 // attention_l (+ pw_mid_l = combine + fc_message_l + residual + PointCN_{l+1}
 // + QKV_{l+1}), and pw_last (combine + fc_message + residual + normalize +
-// classifier).  The pointwise products run on v_mfma_f32_32x32x2_f32 (exact
-// fp32 fma chains); their Q/K/V epilogues write the fp16 hi/lo splits that the
-// attention consumes.
+// classifier).  The pointwise products run on v_mfma_f32_32x32x16_f16 with the
+// 3-product split of attention_h3.hpp (activations split as read from LDS,
+// weights pre-split and power-of-two scaled at pack time); their Q/K/V
+// epilogues write the fp16 hi/lo splits that the attention consumes.
 //
 // Attention (attention_h3.hpp; flash-style, never materialising the N x N
 // logits): 3 fp16 MFMAs per fp32 product (hi.hi + hi.lo + lo.hi, 22-bit
@@ -26,18 +27,42 @@
 namespace pdsc {
 
 // ============================================================ weight packing
+// Per-layer power-of-two scale: max|W| 2^s <= 2^14 keeps hi and (for all but
+// the weights 2^-17 below the layer's largest) lo in fp16's normal range.
+__global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w, int n, float *__restrict__ sc) {
+    __shared__ float part[4];
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = fmaxf(fmaxf(part[0], part[1]), fmaxf(part[2], part[3]));
+        int ex = 0;
+        if (m > 0.0f && m < INFINITY) frexpf(m, &ex);  // m < 2^ex
+        const int sh = max(-100, min(100, 14 - ex));
+        sc[0] = ldexpf(1.0f, -sh);
+        sc[1] = ldexpf(1.0f, sh);
+    }
+}
+
+// W [out][in] (torch Conv1d weight) -> hi / lo fp16 planes of W * 2^s, same
+// [out][in] order: lane (h, n) of a 32x32x16 MFMA reads 8 consecutive inputs of
+// output n as one 16-B load.  BN folded as torch-CPU eval folds it.
 __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__restrict__ b,
                                   const float *__restrict__ bn_w, const float *__restrict__ bn_b,
                                   const float *__restrict__ bn_rm, const float *__restrict__ bn_rv,
                                   int in, int out, float *__restrict__ dw, float *__restrict__ db,
-                                  float *__restrict__ da, float *__restrict__ dbeta) {
+                                  float *__restrict__ da, float *__restrict__ dbeta,
+                                  const float *__restrict__ sc) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = in * out;
     if (i < total) {
-        const int e = i & 3, lane = (i >> 2) & 63, rest = i >> 8;  // rest = jt*(in/8) + g
-        const int g = rest % (in / 8), jt = rest / (in / 8);
-        const int row = jt * 32 + (lane & 31), col = (lane >> 5) * (in / 2) + 4 * g + e;
-        dw[i] = w[row * in + col];
+        _Float16 *wh = reinterpret_cast<_Float16 *>(dw), *wl = wh + total;
+        _Float16 hi, lo;
+        split_h(w[i] * sc[1], hi, lo);
+        wh[i] = hi;
+        wl[i] = lo;
     }
     if (i < out) {
         db[i] = b[i];
@@ -61,10 +86,11 @@ __global__ void copy_kernel(const float *__restrict__ s, float *__restrict__ d, 
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
                              const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
-                             float *dst_b, float *dst_a, float *dst_beta, hipStream_t s) {
+                             float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s) {
     const int n = in * out;
+    hipLaunchKernelGGL(wscale_kernel, dim3(1), dim3(256), 0, s, w, n, dst_scale);
     hipLaunchKernelGGL(pack_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, b, bn_w, bn_b,
-                       bn_rm, bn_rv, in, out, dst_w, dst_b, dst_a, dst_beta);
+                       bn_rm, bn_rv, in, out, dst_w, dst_b, dst_a, dst_beta, dst_scale);
     return hipGetLastError();
 }
 
@@ -160,34 +186,60 @@ enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
 constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
 constexpr int IN_MAX = 16;  // layer0 input width held in registers
 
-template <int IN, int EPI, int NRT>
-PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off,
-                         int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid, int lane) {
+// The wave's weight panel for output tile ct: per 16-input k-step, the hi and
+// lo fragments (lane (h, n): inputs 16 ks + 8h .. +7 of output 32 ct + n).
+template <int IN, int OUT>
+PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int ct, int lane, f16x8 *wh,
+                          f16x8 *wl) {
+    const _Float16 *Wh = reinterpret_cast<const _Float16 *>(pk + off.w);
+    const _Float16 *Wl = Wh + (size_t)OUT * IN;
+    const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 8 * (lane >> 5);
+#pragma unroll
+    for (int ks = 0; ks < IN / 16; ++ks) {
+        wh[ks] = *reinterpret_cast<const f16x8 *>(Wh + rowo + 16 * ks);
+        wl[ks] = *reinterpret_cast<const f16x8 *>(Wl + rowo + 16 * ks);
+    }
+}
+
+// 8 consecutive fp32 activations (LDS, 16-B aligned) -> hi / lo fp16 fragments
+PDSC_DEV void split8(const float *x, f16x8 &hi, f16x8 &lo) {
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(x), b = *reinterpret_cast<const f32x4 *>(x + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        _Float16 p, q;
+        split_h(a[e], p, q);
+        hi[e] = p;
+        lo[e] = q;
+        split_h(b[e], p, q);
+        hi[4 + e] = p;
+        lo[4 + e] = q;
+    }
+}
+
+// One 32-output tile of Y = epi(X W^T + b) for NRT row tiles, on the fp16
+// matrix cores with the 3-product split (attention_h3.hpp): activations split
+// as they are read from LDS, weights pre-split and pre-scaled by 2^s (the
+// accumulator is scaled back by the exact 2^-s before the bias).
+template <int IN, int OUT, int EPI, int NRT>
+PDSC_DEV void dense_tile_w(const float *X, int xstr, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
+                           const DenseOff &off, int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid,
+                           int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
 #pragma unroll
     for (int i = 0; i < NRT; ++i) acc[i] = zero16();
-    const float *xp = X + (rt0 * 32 + l32) * xstr + h * (IN / 2);
-    const f32x4 *wp = reinterpret_cast<const f32x4 *>(pk + off.w) + (size_t)ct * (IN / 8) * 64 + lane;
-    f32x4 wbuf[IN / 8];  // the wave's whole weight panel, issued up front
+    const float *xp = X + (rt0 * 32 + l32) * xstr + 8 * h;
 #pragma unroll
-    for (int g = 0; g < IN / 8; ++g) wbuf[g] = wp[g * 64];
-    // keep the scheduler from sinking the loads next to their uses (each would
-    // then expose a full L2 round trip every 8 MFMAs); waits stay counted
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int g = 0; g < IN / 8; ++g) {
-        const f32x4 wb = wbuf[g];
+    for (int ks = 0; ks < IN / 16; ++ks) {
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
-            const f32x4 xa = *reinterpret_cast<const f32x4 *>(xp + i * 32 * xstr + 4 * g);
-            acc[i] = mfma32(xa[0], wb[0], acc[i]);
-            acc[i] = mfma32(xa[1], wb[1], acc[i]);
-            acc[i] = mfma32(xa[2], wb[2], acc[i]);
-            acc[i] = mfma32(xa[3], wb[3], acc[i]);
+            f16x8 xh, xl;
+            split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
+            acc[i] = mfma_h3(xh, xl, wh[ks], wl[ks], acc[i]);
         }
     }
     const int j = ct * 32 + l32;
+    const float inv = pk[off.scale];
     const float bias = pk[off.bias + j];
     const float al = pk[off.alpha + j], be = pk[off.beta + j];
 #pragma unroll
@@ -195,12 +247,23 @@ PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk,
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (rt0 + i) * 32 + acc_row(r, h);
-            float y = acc[i][r] + bias;
+            float y = acc[i][r] * inv + bias;
             if (EPI == EPI_BN_RELU) y = fmaxf(y * al + be, 0.0f);  // eval BN as torch folds it, ReLU
             if (EPI == EPI_RELU) y = fmaxf(y, 0.0f);
             if (EPI == EPI_RESID) y = resid[row * CH + j] + y;      // res = feat + message (:44)
             Y[row * ystr + j] = y;
         }
+}
+
+template <int IN, int OUT, int EPI, int NRT>
+PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off,
+                         int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid, int lane) {
+    f16x8 wh[IN / 16], wl[IN / 16];  // the wave's whole weight panel, issued up front
+    load_wpanel<IN, OUT>(pk, off, ct, lane, wh, wl);
+    // keep the scheduler from sinking the loads next to their uses (each would
+    // then expose a full L2 round trip per k-step); waits stay counted
+    asm volatile("" ::: "memory");
+    dense_tile_w<IN, OUT, EPI, NRT>(X, xstr, wh, wl, pk, off, rt0, ct, Y, ystr, resid, lane);
 }
 
 // Q/K/V projections (Conv1d 128 -> 128 + bias, :36-38) of the PT-point tile,
@@ -214,27 +277,22 @@ PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk,
 enum SplitMode { SPLIT_Q = 0, SPLIT_K = 1, SPLIT_V = 2 };
 
 template <int MODE>
-PDSC_DEV void dense_split(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, int ct,
-                          _Float16 *__restrict__ dst, int p0, int lane) {
+PDSC_DEV void dense_split(const float *X, int xstr, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
+                          const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[2] = {zero16(), zero16()};
-    const float *xp = X + l32 * xstr + h * (CH / 2);
-    const f32x4 *wp = reinterpret_cast<const f32x4 *>(pk + off.w) + (size_t)ct * (CH / 8) * 64 + lane;
-    f32x4 wbuf[CH / 8];
+    const float *xp = X + l32 * xstr + 8 * h;
 #pragma unroll
-    for (int g = 0; g < CH / 8; ++g) wbuf[g] = wp[g * 64];
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int g = 0; g < CH / 8; ++g) {
-        const f32x4 wb = wbuf[g];
+    for (int ks = 0; ks < CH / 16; ++ks) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const f32x4 xa = *reinterpret_cast<const f32x4 *>(xp + i * 32 * xstr + 4 * g);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                acc[i] = MODE == SPLIT_V ? mfma32(xa[e], wb[e], acc[i]) : mfma32(wb[e], xa[e], acc[i]);
+            f16x8 xh, xl;
+            split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
+            acc[i] = MODE == SPLIT_V ? mfma_h3(xh, xl, wh[ks], wl[ks], acc[i])
+                                     : mfma_h3(wh[ks], wl[ks], xh, xl, acc[i]);
         }
     }
+    const float inv = pk[off.scale];
     if constexpr (MODE == SPLIT_V) {
         const int c = ct * 32 + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
         const float bias = pk[off.bias + c];
@@ -247,7 +305,7 @@ PDSC_DEV void dense_split(const float *X, int xstr, const float *__restrict__ pk
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     _Float16 a, b;
-                    split_h(acc[i][8 * s + e] + bias, a, b);
+                    split_h(acc[i][8 * s + e] * inv + bias, a, b);
                     hi[e] = a;
                     lo[e] = b;
                 }
@@ -270,7 +328,7 @@ PDSC_DEV void dense_split(const float *X, int xstr, const float *__restrict__ pk
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     _Float16 a, b;
-                    split_h(acc[i][8 * s + e] + bias[8 * s + e], a, b);
+                    split_h(acc[i][8 * s + e] * inv + bias[8 * s + e], a, b);
                     hi[e] = a;
                     lo[e] = b;
                 }
@@ -288,10 +346,10 @@ PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, co
                       int ystr, const float *__restrict__ resid, int wave, int lane) {
     constexpr int NCT = OUT / 32;
     if constexpr (NCT >= 4) {
-        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, EPI, 2>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
+        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, OUT, EPI, 2>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
     } else {
         const int rt = wave & 1, ct = wave >> 1;
-        if (ct < NCT) dense_tile<IN, EPI, 1>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
+        if (ct < NCT) dense_tile<IN, OUT, EPI, 1>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
     }
 }
 
@@ -322,12 +380,22 @@ constexpr size_t PW_LDS = (size_t)(2 * PT * S132) * sizeof(float);
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                       _Float16 *__restrict__ V, int p0, int tid, int wave, int lane) {
-    dense64<CH, CH, EPI_BN_RELU>(Xin, S132, pk, d.pcn, Xout, S132, nullptr, wave, lane);
+    // four 128 -> 128 products with the same wave -> output-tile map (ct = wave):
+    // each one's weight panel is fetched while the previous one computes
+    f16x8 ah[CH / 16], al[CH / 16], bh[CH / 16], bl[CH / 16];
+    load_wpanel<CH, CH>(pk, d.pcn, wave, lane, ah, al);
+    load_wpanel<CH, CH>(pk, d.q, wave, lane, bh, bl);
+    asm volatile("" ::: "memory");
+    dense_tile_w<CH, CH, EPI_BN_RELU, 2>(Xin, S132, ah, al, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
     __syncthreads();
+    load_wpanel<CH, CH>(pk, d.k, wave, lane, ah, al);
+    asm volatile("" ::: "memory");
     store_rows(Xout, S132, feat, p0, PT, tid);
-    dense_split<SPLIT_Q>(Xout, S132, pk, d.q, wave, Q, p0, lane);
-    dense_split<SPLIT_K>(Xout, S132, pk, d.k, wave, K, p0, lane);
-    dense_split<SPLIT_V>(Xout, S132, pk, d.v, wave, V, p0, lane);
+    dense_split<SPLIT_Q>(Xout, S132, bh, bl, pk, d.q, wave, Q, p0, lane);
+    load_wpanel<CH, CH>(pk, d.v, wave, lane, bh, bl);
+    asm volatile("" ::: "memory");
+    dense_split<SPLIT_K>(Xout, S132, ah, al, pk, d.k, wave, K, p0, lane);
+    dense_split<SPLIT_V>(Xout, S132, bh, bl, pk, d.v, wave, V, p0, lane);
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.

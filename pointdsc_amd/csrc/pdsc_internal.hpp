@@ -34,10 +34,13 @@ inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 //   W  : OUT*IN floats in MFMA fragment order:
 //        Wpk[((jt*(IN/8) + g)*64 + lane)*4 + e] = W[jt*32 + (lane&31)][(lane>>5)*(IN/2) + 4g + e]
 //   bias[OUT], alpha[OUT], beta[OUT]   (alpha=1, beta=0 when no BN)
+// A dense layer in the packed blob: W as two fp16 planes [out][in] (hi, lo:
+// W * 2^s = hi + lo, s chosen per layer so max|W| 2^s <= 2^14) occupying the
+// out*in floats at w, then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
 struct DenseOff {
-    size_t w, bias, alpha, beta;
+    size_t w, bias, alpha, beta, scale;
 };
-inline size_t dense_floats(int in, int out) { return (size_t)out * in + 3 * (size_t)out; }
+inline size_t dense_floats(int in, int out) { return (size_t)out * in + 3 * (size_t)out + 4; }
 
 struct LayerOff {
     DenseOff pcn, fc0, fc3, fc6, q, k, v;
@@ -65,6 +68,8 @@ inline DenseOff dense_at(size_t &o, int in, int out) {
     d.beta = o;
     o += out;
     o = (o + 3) & ~size_t(3);
+    d.scale = o;
+    o += 4;
     return d;
 }
 
@@ -110,7 +115,7 @@ hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
                              const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
-                             float *dst_b, float *dst_a, float *dst_beta, hipStream_t s);
+                             float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s);
 hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 
 // Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
