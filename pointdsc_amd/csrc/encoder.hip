@@ -276,18 +276,37 @@ PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk,
 //     positions of the point tile: 16-B stores into the tile's V planes.
 enum SplitMode { SPLIT_Q = 0, SPLIT_K = 1, SPLIT_V = 2 };
 
+// The PT x 128 activation tile split once into hi / lo fp16 in LDS (row r:
+// 16 hi chunks of 16 B then 16 lo chunks, chunk c stored at c ^ (r & 15) so a
+// fragment read -- 32 rows, one chunk each -- is conflict-free).  Shared by the
+// Q, K and V products instead of re-splitting per wave and per product.
+constexpr int XS_ROWB = 2 * CH * 2;  // bytes per split row
+PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
+    const int r = tid >> 2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = (tid & 3) * 4 + q;
+        f16x8 hi, lo;
+        split8(X + r * xstr + 8 * c, hi, lo);
+        const int o = r * XS_ROWB + 16 * (c ^ (r & 15));
+        *reinterpret_cast<f16x8 *>(Xs + o) = hi;
+        *reinterpret_cast<f16x8 *>(Xs + o + CH * 2) = lo;
+    }
+}
+
 template <int MODE>
-PDSC_DEV void dense_split(const float *X, int xstr, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
+PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
                           const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[2] = {zero16(), zero16()};
-    const float *xp = X + l32 * xstr + 8 * h;
 #pragma unroll
     for (int ks = 0; ks < CH / 16; ++ks) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            f16x8 xh, xl;
-            split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
+            const int r = 32 * i + l32;
+            const char *xr = Xs + r * XS_ROWB + 16 * ((2 * ks + h) ^ (r & 15));
+            const f16x8 xh = *reinterpret_cast<const f16x8 *>(xr);
+            const f16x8 xl = *reinterpret_cast<const f16x8 *>(xr + CH * 2);
             acc[i] = MODE == SPLIT_V ? mfma_h3(xh, xl, wh[ks], wl[ks], acc[i])
                                      : mfma_h3(wh[ks], wl[ks], xh, xl, acc[i]);
         }
@@ -387,15 +406,18 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
     load_wpanel<CH, CH>(pk, d.q, wave, lane, bh, bl);
     asm volatile("" ::: "memory");
     dense_tile_w<CH, CH, EPI_BN_RELU, 2>(Xin, S132, ah, al, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
-    __syncthreads();
+    __syncthreads();  // Xout complete; Xin is dead and now holds the split copy of Xout
+    char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
+    split_tile(Xout, S132, Xs, tid);
     load_wpanel<CH, CH>(pk, d.k, wave, lane, ah, al);
     asm volatile("" ::: "memory");
     store_rows(Xout, S132, feat, p0, PT, tid);
-    dense_split<SPLIT_Q>(Xout, S132, bh, bl, pk, d.q, wave, Q, p0, lane);
+    __syncthreads();
+    dense_split<SPLIT_Q>(Xs, bh, bl, pk, d.q, wave, Q, p0, lane);
     load_wpanel<CH, CH>(pk, d.v, wave, lane, bh, bl);
     asm volatile("" ::: "memory");
-    dense_split<SPLIT_K>(Xout, S132, ah, al, pk, d.k, wave, K, p0, lane);
-    dense_split<SPLIT_V>(Xout, S132, bh, bl, pk, d.v, wave, V, p0, lane);
+    dense_split<SPLIT_K>(Xs, ah, al, pk, d.k, wave, K, p0, lane);
+    dense_split<SPLIT_V>(Xs, bh, bl, pk, d.v, wave, V, p0, lane);
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
