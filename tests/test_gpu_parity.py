@@ -134,8 +134,9 @@ def test_debug_outputs_match_reference(name, gpu_device):
 
 
 def test_batched_equals_single(gpu_device):
-    """B pairs in one call == B single-pair calls (labels bitwise; poses to
-    fp32 rounding -- the attention split-K depends on B)."""
+    """B pairs in one call == B single-pair calls (labels bitwise; poses within
+    the north-star pose tolerance: the attention's split-K over keys depends on
+    B, so the softmax partials combine in a different fp32 order)."""
     from pointdsc_amd.synthetic import synthetic_batch
     g = load_golden("rel_1k")
     m = _model(g, gpu_device)
@@ -146,7 +147,7 @@ def test_batched_equals_single(gpu_device):
         r = m({"corr_pos": corr[i:i + 1], "src_keypts": src[i:i + 1], "tgt_keypts": tgt[i:i + 1],
                "testing": True})
         assert torch.equal(r["final_labels"][0], Lb[i])
-        np.testing.assert_allclose(r["final_trans"][0].cpu().numpy(), T[i].cpu().numpy(), atol=1e-5)
+        np.testing.assert_allclose(r["final_trans"][0].cpu().numpy(), T[i].cpu().numpy(), atol=POSE_ATOL)
 
 
 def test_graph_replay_equals_eager(gpu_device):
