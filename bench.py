@@ -297,11 +297,25 @@ def main():
             st5, _ = ev5.stage_means()
             S5, k5 = int(N5 * 0.1), min(40, N5 - 1)
             pb = P5 * path_bytes(N5, S5, k5)
+            # measured HBM bytes of the same stages from the committed profile (launch
+            # shapes as api.hip launches them at this N, P)
+            nt5 = (N5 + 63) // 64
+            shapes = [("compat_packed_kernel", nt5 * (nt5 + 1) // 2 * P5 * 256),
+                      ("knn_dist_kernel", ((N5 + 31) // 32 + 4) // 5 * ((S5 + 127) // 128) * P5 * 256),
+                      ("split_rows_kernel", None),
+                      (f"knn_select_kernel<{next(r for r in (16, 32, 48, 64, 80, 96, 128, 0) if r == 0 or r * 64 >= N5)}>",
+                       (S5 + 3) // 4 * P5 * 256),
+                      ("nsm_local_kernel", S5 * P5 * 256), ("nsm_finish_kernel", S5 * P5 * 64)]
+            profs = [profiled(kname, g) for kname, g in shapes if g is not None]
+            path_traffic = (sum(pr["hbm_bytes"] for pr in profs)
+                            if profs and all(pr and pr["hbm_bytes"] is not None for pr in profs) else None)
             t_path = st5["compat"] + st5["seed_knn"] + st5["nsm"]
             ach = pb / (t_path * 1e-3) / 1e9
             roofline_path = {"stages": "compat + seed_knn + nsm", "bound": "hbm", "achieved": round(ach, 1),
                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
-                             "traffic": None, "num_corr": N5, "pairs": P5, "path_ms": round(t_path, 4),
+                             "traffic": path_traffic, "traffic_note": "HBM bytes of the stages' kernels per forward "
+                             "(rocprofv3 2*FETCH_SIZE+WRITE_SIZE, profiles/traffic_current.json)",
+                             "num_corr": N5, "pairs": P5, "path_ms": round(t_path, 4),
                              "bytes_per_pair": path_bytes(N5, S5, k5),
                              "stage_ms": {k: round(v, 4) for k, v in st5.items()},
                              "forward_ms": round(fwd5 * 1e3, 3),
@@ -321,7 +335,9 @@ def main():
             d1s = synthetic_batch(1, Ns, seed=9000 + rank, preset=args.preset)
             cs, ss, ts = (torch.from_numpy(d1s[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
             sm_ms = event_time(lambda: SM(cs, ss, ts, inlier_threshold=p["inlier_threshold"]), 5, stream)
+            mv_prof = profiled("sm_matvec_kernel", (Ns + 3) // 4 * 256)
             roofline_sm = {"kernel": "sm_matvec_kernel", "bound": "hbm", "num_corr": Ns,
+                           "traffic": mv_prof and mv_prof["hbm_bytes"], "profile": mv_prof,
                            "achieved": round(mvb / (mv_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                            "frac": round(mvb / (mv_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4), "launch_ms": round(mv_ms, 4),
                            "bytes_per_launch": mvb,
