@@ -217,14 +217,15 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
         }
         float p[16];
         float mx = -INFINITY;
-        const bool tail = key0 + 32 > N;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float x = mv[r] * (S[r] * scale);  // (:39) then * M (:41); 0, not -inf, off-support
-            if (tail && key0 + acc_row(r, h) >= N) x = -INFINITY;
-            p[r] = x;
-            mx = fmaxf(mx, x);
+        for (int r = 0; r < 16; ++r) p[r] = mv[r] * (S[r] * scale);  // (:39) then * M (:41); 0, not -inf, off-support
+        if (key0 + 32 > N) {  // wave-uniform: only the last key tile has padding keys
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (key0 + acc_row(r, h) >= N) p[r] = -INFINITY;
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, p[r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32));
         if (__any(mx > m_run + H3_DEFER)) {  // wave-uniform re-base of the running max
             const float m_new = fmaxf(m_run, mx);
