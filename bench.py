@@ -11,13 +11,17 @@ timed region and a max-reduce of the elapsed time.
 
 Prints ONE JSON line (rank 0).  Also measured live with HIP events on the
 stream the kernels run on:
-  roofline      -- the dominant kernel (SCNonlocal attention), fp32 MFMA bound
+  roofline      -- the dominant kernel (SCNonlocal attention), MFMA bound; its fp32
+                   products run as 3 fp16 MFMAs, so the peak is 2500/3 TFLOP/s
   roofline_hbm  -- the a1 compatibility kernel, HBM-write bound
   roofline_path -- SURVEY 8(d)'s target: the compat + seed-kNN + NSM power-iteration
                    stages at N=5000 (stage events inside the forward), HBM bound,
                    priced with the algorithmic bytes B(N) = 24N + 4N^2 + S*k*(C+6)*4 + 4*S*k
   stages        -- per-stage ms of the headline forward (pdsc_forward_timing events)
+  roofline_sm   -- SURVEY 8(f) row 3: the SM baseline's matrix-vector product at N=5000, HBM bound
   single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph
+Each roofline's `traffic` is the HBM bytes per launch of the same kernel at the
+same launch shape from the committed rocprofv3 profile (profiles/traffic_current.json).
   cpu_baseline  -- the CPU oracle (oracle/, numpy + C) on a bounded sample
 """
 import argparse
