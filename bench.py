@@ -309,7 +309,7 @@ def main():
                       ("split_rows_kernel", None),
                       (f"knn_select_kernel<{next(r for r in (16, 32, 48, 64, 80, 96, 128, 0) if r == 0 or r * 64 >= N5)}>",
                        (S5 + 3) // 4 * P5 * 256),
-                      ("nsm_local_kernel", S5 * P5 * 256), ("nsm_finish_kernel", S5 * P5 * 64)]
+                      ("nsm_seed_kernel", (S5 + 3) // 4 * P5 * 256), ("nsm_finish_kernel", S5 * P5 * 64)]
             profs = [profiled(kname, g) for kname, g in shapes if g is not None]
             path_traffic = (sum(pr["hbm_bytes"] for pr in profs)
                             if profs and all(pr and pr["hbm_bytes"] is not None for pr in profs) else None)

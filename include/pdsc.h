@@ -152,7 +152,7 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
  * w = v / (sum v + 1e-6).  Replaces models/PointDSC.py:257-282, :338-358.
  * sigma_dev / sigma_d_dev: device scalars (learned sigma, sigma_spat).
  * weights [B,S,k]; iters_used [B] int32 (may be NULL).                      */
-size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t S, int32_t k, int32_t num_iterations);
+size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t N, int32_t S, int32_t k, int32_t num_iterations);
 int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt,
                          const int32_t *knn, int32_t B, int32_t N, int32_t C, int32_t S, int32_t k,
                          int32_t num_iterations, const float *sigma_dev, const float *sigma_d_dev,

@@ -55,7 +55,7 @@ _PROTOS = {
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
     "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
-    "pdsc_nsm_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
+    "pdsc_nsm_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32, c_int32]),
     "pdsc_nsm_weights": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                    vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_rigid_transform_3d": (c_int32, [vp, vp, vp, c_int32, c_int32, vp, vp]),

@@ -134,25 +134,31 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
 }
 
 struct NsmBufs {
-    float *hist, *weights, *T;
+    float *hist, *weights;
+    _Float16 *ns;  // split normed copy (standalone API only; the forward passes pw_last's)
     unsigned *mask;
 };
 
-NsmBufs carve_nsm(Carve &c, int B, int S, int k, int T) {
+NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
     NsmBufs n;
-    n.T = c.take<float>((size_t)B * S * k * k);
+    n.ns = own_split ? c.take<_Float16>((size_t)B * N * 2 * CH) : nullptr;
     n.hist = c.take<float>((size_t)B * S * std::max(T, 1) * k);
     n.mask = c.take<unsigned>((size_t)B);
     n.weights = c.take<float>((size_t)B * S * k);
     return n;
 }
 
-int run_nsm(const float *normed, const float *src, const float *tgt, const int *knn, int B, int N,
-            int S, int k, int T, const float *sigma, const float *sigma_d, const NsmBufs &nb,
+// normed_s: the split normed copy, or NULL to build it here from normed
+int run_nsm(const float *normed, const _Float16 *normed_s, const float *src, const float *tgt, const int *knn,
+            int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d, const NsmBufs &nb,
             float *weights, int *iters, hipStream_t s) {
     HIPCHK(hipMemsetAsync(nb.mask, 0xff, sizeof(unsigned) * B, s));
+    if (!normed_s) {
+        HIPCHK(launch_split_rows(normed, (size_t)B * N, nb.ns, s));
+        normed_s = nb.ns;
+    }
     if (T > 0)
-        HIPCHK(launch_nsm_power(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.T, nb.hist, nb.mask, s));
+        HIPCHK(launch_nsm_seed(normed_s, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
     HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, weights, iters, s));
     return PDSC_OK;
 }
@@ -177,7 +183,7 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.seeds = c.take<int>((size_t)d.B * d.S);
     f.kdist = c.take<float>((size_t)d.B * d.S * d.N);
     f.knn = c.take<int>((size_t)d.B * d.S * d.k);
-    f.nsm = carve_nsm(c, d.B, d.S, d.k, d.T);
+    f.nsm = carve_nsm(c, d.B, d.N, d.S, d.k, d.T, false);
     f.weights = f.nsm.weights;
     f.seed_trans = c.take<float>((size_t)d.B * d.S * 16);
     f.counts = c.take<int>((size_t)d.B * d.S);
@@ -429,9 +435,9 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
 }
 
 // ----------------------------------------------------------------- a7-a8
-size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t S, int32_t k, int32_t T) {
+size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t N, int32_t S, int32_t k, int32_t T) {
     Carve c(nullptr);
-    carve_nsm(c, B, S, k, T);
+    carve_nsm(c, B, N, S, k, T, true);
     return c.off;
 }
 
@@ -443,10 +449,10 @@ int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt
     if (!normed || !src || !tgt || !knn || !sigma || !sigma_d || !weights || !ws)
         return fail(PDSC_ERR_ARG, "null pointer");
     if (B < 1 || S < 1 || k < 1 || k > 64 || T < 0 || T > 31) return fail(PDSC_ERR_ARG, "B=%d S=%d k=%d T=%d", B, S, k, T);
-    RET_IF(need_ws(ws_bytes, pdsc_nsm_workspace_bytes(B, S, k, T)));
+    RET_IF(need_ws(ws_bytes, pdsc_nsm_workspace_bytes(B, N, S, k, T)));
     Carve c(ws);
-    NsmBufs nb = carve_nsm(c, B, S, k, T);
-    return run_nsm(normed, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb, weights, iters, S_(stream));
+    NsmBufs nb = carve_nsm(c, B, N, S, k, T, true);
+    return run_nsm(normed, nullptr, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb, weights, iters, S_(stream));
 }
 
 // -------------------------------------------------------------------- a9
@@ -542,7 +548,7 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
     STAGE(4);
     // a7-a8 (:257-282)
-    RET_IF(run_nsm(f.normed, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
+    RET_IF(run_nsm(f.normed, f.normed_s, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
                    nullptr, s));
     STAGE(5);
     // a9-a10 (:287-335)

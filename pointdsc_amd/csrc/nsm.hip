@@ -5,9 +5,9 @@
 //   knn_select   a6  topk(k+1, smallest)[1:] per seed row (one wave per seed,
 //                    row in registers): lane-minimum threshold + compaction +
 //                    (key, index) ranking; radix-select fallback
-//   nsm_local    a7-a8  gather k neighbours, k x k feature*spatial consistency T
-//                    in LDS, then all num_iterations power iterates + per-iterate
-//                    allclose flags (T never written to HBM)
+//   nsm_seed     a7-a8  one wave per seed: k x k feature Gram on the fp16
+//                    matrix cores (3-product split), T = F o S in LDS, then all
+//                    num_iterations power iterates + per-iterate allclose flags
 //   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
 //                    is allclose (torch.allclose over the whole batch, :354)
 //   hypotheses   a9-a10  weighted Kabsch per seed (fp64 3x3 SVD on device) +
@@ -403,7 +403,6 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
 
 // -------------------------------------------------------------- a7-a8 NSM
 constexpr int KMAX = 64;
-constexpr int FSTR = CH + 4;
 
 // Power iteration of one seed's k x k matrix (models/PointDSC.py:347-358), one
 // wave: lane a holds row a of T in registers, v is broadcast from LDS 4 entries
@@ -440,109 +439,116 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
     return flags;
 }
 
-// nsm_local: one workgroup per (seed, pair) builds the k x k matrix T of the
-// seed's neighbourhood in LDS, then its first wave runs all T power iterates
-// (hist[b][s][t][a]) and AND-s the per-iterate allclose bits into pair_mask[b]
-// -- T never leaves the CU.
-__global__ __launch_bounds__(256) void nsm_local_kernel(const float *__restrict__ normed,
-                                                        const float *__restrict__ src,
-                                                        const float *__restrict__ tgt,
-                                                        const int *__restrict__ knn, int N, int S,
-                                                        int k, int T, const float *__restrict__ sigma_p,
-                                                        const float *__restrict__ sigma_d_p,
-                                                        float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
-    // dynamic LDS sized by k (nsm_local_lds_bytes): F [kp][FSTR] then T [k][k+1]
-    extern __shared__ __attribute__((aligned(16))) float nsm_dyn[];
-    __shared__ float P[KMAX][6];
-    __shared__ int nidx[KMAX];
-    __shared__ __attribute__((aligned(16))) float vb[KMAX];
-    float *F = nsm_dyn;
-    float *Tl = nsm_dyn + (size_t)((k + 1) & ~1) * FSTR;
+// nsm_seed_kernel: one WAVE per (seed, pair), 4 seeds per workgroup.  The
+// k x k feature Gram matrix of the seed's neighbourhood comes from the fp16
+// matrix cores with the 3-product split (attention_h3.hpp), its operands read
+// straight from the split normed copy ns [B][N][2][128] (the same bytes the
+// seed kNN reads) into registers: tiles (0,0), (0,1), (1,1) of 32 x 32 for
+// k <= 64.  T = F o S (diag 0, :257-278) goes to the wave's slice of LDS, each
+// unordered pair evaluated once and mirrored (T exactly symmetric), then the
+// same wave runs the power iteration.  No workgroup barriers: waves are
+// independent.
+constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
+
+__global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restrict__ ns,
+                                                       const float *__restrict__ src,
+                                                       const float *__restrict__ tgt,
+                                                       const int *__restrict__ knn, int N, int S, int k, int T,
+                                                       const float *__restrict__ sigma_p,
+                                                       const float *__restrict__ sigma_d_p,
+                                                       float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
+    extern __shared__ __attribute__((aligned(16))) float nsm_sdyn[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.y, s = blockIdx.x * 4 + wave;
+    if (s >= S) return;  // wave-uniform
     const int tls = k + 1;
-    const int b = blockIdx.y, s = blockIdx.x, tid = threadIdx.x;
+    float *Tl = nsm_sdyn + (size_t)wave * (k * tls + KMAX * NSM_PSTR + KMAX);
+    float *P = Tl + k * tls;  // [KMAX][NSM_PSTR]: src xyz, tgt xyz
+    float *vb = P + KMAX * NSM_PSTR;
     const float sig = sigma_p[0], sd = sigma_d_p[0];
     const float sig2 = sig * sig, sd2 = sd * sd;
-    if (tid < k) nidx[tid] = min(max(knn[((size_t)b * S + s) * k + tid], 0), N - 1);
-    __syncthreads();
-    const float *Fb = normed + (size_t)b * N * CH;
-    const int kp = (k + 1) & ~1;  // rows padded to even (zero features) for 2x2 blocking
-    for (int e = tid; e < kp * (CH / 4); e += 256) {
-        const int a = e / (CH / 4), c4 = e % (CH / 4);
-        *reinterpret_cast<f32x4 *>(&F[a * FSTR + 4 * c4]) =
-            (a < k) ? *reinterpret_cast<const f32x4 *>(Fb + (size_t)nidx[a] * CH + 4 * c4) : f32x4{0, 0, 0, 0};
+    const float rsig2 = 1.0f / sig2, rsd2 = 1.0f / sd2;
+    const int *kr = knn + ((size_t)b * S + s) * k;
+    const int idx = min(max(kr[lane < k ? lane : 0], 0), N - 1);
+    {
+        const float *ps = src + ((size_t)b * N + idx) * 3, *pt = tgt + ((size_t)b * N + idx) * 3;
+        *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{ps[0], ps[1], ps[2], pt[0]};
+        *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{pt[1], pt[2], 0.0f, 0.0f};
     }
-    for (int e = tid; e < k * 6; e += 256) {
-        const int a = e / 6, c = e % 6;
-        const float *base = (c < 3 ? src : tgt) + ((size_t)b * N + nidx[a]) * 3;
-        P[a][c] = base[c % 3];
-    }
-    __syncthreads();
-    // local consistency (models/PointDSC.py:257-278).  The feature Gram matrix is
-    // symmetric: each thread owns one 2x2 block of its upper triangle (4 dot
-    // products sharing 4 row reads), and writes both mirrored entries.
-    const int nbk = kp / 2;
-    for (int t = tid; t < nbk * (nbk + 1) / 2; t += 256) {
-        int bi = 0, rem = t;
-        while (rem >= nbk - bi) {
-            rem -= nbk - bi;
-            ++bi;
-        }
-        const int bj = bi + rem;
-        const int a0 = 2 * bi, c0 = 2 * bj;
-        const f32x4 *fa0 = reinterpret_cast<const f32x4 *>(&F[a0 * FSTR]);
-        const f32x4 *fa1 = reinterpret_cast<const f32x4 *>(&F[(a0 + 1) * FSTR]);
-        const f32x4 *fc0 = reinterpret_cast<const f32x4 *>(&F[c0 * FSTR]);
-        const f32x4 *fc1 = reinterpret_cast<const f32x4 *>(&F[(c0 + 1) * FSTR]);
-        f32x4 d00 = {0, 0, 0, 0}, d01 = d00, d10 = d00, d11 = d00;
-#pragma unroll 4
-        for (int i = 0; i < CH / 4; ++i) {
-            const f32x4 x0 = fa0[i], x1 = fa1[i], y0 = fc0[i], y1 = fc1[i];
+    const _Float16 *F = ns + (size_t)b * N * 2 * CH;
+    auto load_frag = [&](int t, f16x8 *fh, f16x8 *fl) {
+        const int row = __shfl(idx, 32 * t + l32);
+        const _Float16 *rp = F + (size_t)row * 2 * CH;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                d00[e] = __builtin_fmaf(x0[e], y0[e], d00[e]);
-                d01[e] = __builtin_fmaf(x0[e], y1[e], d01[e]);
-                d10[e] = __builtin_fmaf(x1[e], y0[e], d10[e]);
-                d11[e] = __builtin_fmaf(x1[e], y1[e], d11[e]);
-            }
+        for (int j = 0; j < 8; ++j) {
+            fh[j] = *reinterpret_cast<const f16x8 *>(rp + 8 * (2 * j + h));
+            fl[j] = *reinterpret_cast<const f16x8 *>(rp + CH + 8 * (2 * j + h));
         }
-        const float dots[4] = {(d00[0] + d00[1]) + (d00[2] + d00[3]), (d01[0] + d01[1]) + (d01[2] + d01[3]),
-                               (d10[0] + d10[1]) + (d10[2] + d10[3]), (d11[0] + d11[1]) + (d11[2] + d11[3])};
+    };
+    f16x8 ah[8], al[8], bh[8], bl[8];
+    const int nt = (k + 31) / 32;
+    load_frag(0, ah, al);
+    if (nt > 1) load_frag(1, bh, bl);
+    __builtin_amdgcn_wave_barrier();  // P visible to the wave
+    // T for one 32 x 32 Gram tile: rows 32 ta + acc_row(r, h), columns 32 tb + l32
+    auto emit = [&](const f32x16 &G, int ta, int tb) {
+        const int c = 32 * tb + l32;
+        const f32x4 pc0 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR);
+        const f32x4 pc1 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR + 4);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int a = a0 + (q >> 1), c = c0 + (q & 1);
-            if (a >= k || c >= k || a > c) continue;  // upper triangle (diagonal block: a <= c)
+        for (int r = 0; r < 16; ++r) {
+            const int a = 32 * ta + acc_row(r, h);
+            if (a >= k || c >= k || (ta == tb && a > c)) continue;  // each unordered pair once
             float val = 0.0f;
             if (a != c) {
-                const float fm = fmaxf(1.0f - (1.0f - dots[q]) / sig2, 0.0f);  // :259
-                float dx = P[a][0] - P[c][0], dy = P[a][1] - P[c][1], dz = P[a][2] - P[c][2];
-                const float ds = sqrtf((dx * dx + dy * dy) + dz * dz);       // :268
-                dx = P[a][3] - P[c][3];
-                dy = P[a][4] - P[c][4];
-                dz = P[a][5] - P[c][5];
-                const float dt = sqrtf((dx * dx + dy * dy) + dz * dz);
+                const f32x4 pa0 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR);
+                const f32x4 pa1 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR + 4);
+                // correctly rounded '/' and sqrtf through their fma-corrected forms
+                // (pdsc_common.hpp; exact for normal operands, within 1 ulp below 2^-96)
+                const float fm = fmaxf(1.0f - cr_div(1.0f - G[r], sig2, rsig2), 0.0f);  // :259
+                float dx = pa0[0] - pc0[0], dy = pa0[1] - pc0[1], dz = pa0[2] - pc0[2];
+                const float ds = cr_sqrt((dx * dx + dy * dy) + dz * dz);    // :268
+                dx = pa0[3] - pc0[3];
+                dy = pa1[0] - pc1[0];
+                dz = pa1[1] - pc1[1];
+                const float dt = cr_sqrt((dx * dx + dy * dy) + dz * dz);
                 const float dd = ds - dt;
-                const float sm = fmaxf(1.0f - (dd * dd) / sd2, 0.0f);        // :270
-                val = fm * sm;                                               // :277 (diag 0, :278)
+                const float sm = fmaxf(1.0f - cr_div(dd * dd, sd2, rsd2), 0.0f);     // :270
+                val = fm * sm;                                            // :277 (diag 0, :278)
             }
             Tl[a * tls + c] = val;
             Tl[c * tls + a] = val;
         }
+    };
+    {
+        f32x16 G = zero16();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) G = mfma_h3(ah[j], al[j], ah[j], al[j], G);
+        emit(G, 0, 0);
     }
-    __syncthreads();
-    if (tid < 64) {
-        const unsigned flags = power_iterate(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, tid);
-        if (tid == 0) atomicAnd(&pair_mask[b], flags);
+    if (nt > 1) {
+        f32x16 G = zero16();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) G = mfma_h3(ah[j], al[j], bh[j], bl[j], G);
+        emit(G, 0, 1);
+        G = zero16();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) G = mfma_h3(bh[j], bl[j], bh[j], bl[j], G);
+        emit(G, 1, 1);
     }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned flags = power_iterate(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
+    if (lane == 0) atomicAnd(&pair_mask[b], flags);
 }
 
-hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
-                            int B, int N, int S, int k, int T, const float *sigma,
-                            const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
-                            hipStream_t s) {
-    (void)Tg;  // T stays in LDS (nsm_local_kernel)
-    const size_t lds = ((size_t)((k + 1) & ~1) * FSTR + (size_t)k * (k + 1)) * sizeof(float);
-    hipLaunchKernelGGL(nsm_local_kernel, dim3(S, B), dim3(256), lds, s, normed, src, tgt, knn, N, S, k, T,
-                       sigma, sigma_d, hist, pair_mask);
+size_t nsm_seed_lds_bytes(int k) { return (size_t)4 * (k * (k + 1) + KMAX * NSM_PSTR + KMAX) * sizeof(float); }
+
+hipError_t launch_nsm_seed(const _Float16 *ns, const float *src, const float *tgt, const int *knn, int B, int N,
+                           int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
+                           unsigned *pair_mask, hipStream_t s) {
+    if (k < 1 || k > KMAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nsm_seed_kernel, dim3((S + 3) / 4, B), dim3(256), nsm_seed_lds_bytes(k), s, ns, src, tgt, knn,
+                       N, S, k, T, sigma, sigma_d, hist, pair_mask);
     return hipGetLastError();
 }
 

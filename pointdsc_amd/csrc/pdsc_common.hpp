@@ -58,6 +58,29 @@ inline float sqrt_ge_threshold(float R) {
     return t;
 }
 
+// Correctly rounded sqrtf for x == 0, +inf or x >= 2^-96 (the caller takes
+// the library sqrtf when a wave holds a smaller positive x): v_sqrt_f32 is
+// within 1 ulp, and the neighbour whose fma residual shows it closer replaces
+// it -- the same correction hipcc's -fhip-fp32-correctly-rounded-divide-sqrt
+// emits, minus the denormal rescaling and class fix-ups this domain needs not.
+PDSC_DEV float cr_sqrt(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float dn = __uint_as_float(__float_as_uint(s) - 1u), up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-dn, s, x), rup = __builtin_fmaf(-up, s, x);
+    float r = rdn <= 0.0f ? dn : s;
+    r = rup > 0.0f ? up : r;
+    return x == 0.0f ? x : r;
+}
+
+// Correctly rounded x / d given rcp = RN(1/d) (Markstein: q = RN(x rcp) is
+// within 1 ulp, the fma remainder is exact, and one fma correction rounds
+// to RN(x / d); x, d normal and no overflow -- d = sigma_d^2 > 0).
+PDSC_DEV float cr_div(float x, float d, float rcp) {
+    const float q = x * rcp;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, rcp, q);
+}
+
 // |v| for a residual vector, same evaluation order as pdist3.
 PDSC_DEV float norm3(float dx, float dy, float dz) {
     return sqrtf(__builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx)));

@@ -153,11 +153,10 @@ hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, i
                            hipStream_t s);
 hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s);
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s);
-// Tg: scratch [B][S][k][k]
-hipError_t launch_nsm_power(const float *normed, const float *src, const float *tgt, const int *knn,
-                            int B, int N, int S, int k, int T, const float *sigma,
-                            const float *sigma_d, float *Tg, float *hist, unsigned *pair_mask,
-                            hipStream_t s);
+// ns: the split normed copy [B][N][2][128] fp16 (as launch_knn_dist reads it)
+hipError_t launch_nsm_seed(const _Float16 *ns, const float *src, const float *tgt, const int *knn, int B, int N,
+                           int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
+                           unsigned *pair_mask, hipStream_t s);
 hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B, int S, int k, int T,
                              float *weights, int *iters_used, hipStream_t s);
 // sums: scratch [B][S][15]

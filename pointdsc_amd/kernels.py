@@ -161,7 +161,7 @@ def nsm_weights(normed, src, tgt, knn, num_iterations, sigma, sigma_d):
     B, N, C = normed.shape
     _, S, k = knn.shape
     L = _lib.load()
-    nb = L.pdsc_nsm_workspace_bytes(B, S, k, int(num_iterations))
+    nb = L.pdsc_nsm_workspace_bytes(B, N, S, k, int(num_iterations))
     ws = _workspace(nb, normed.device)
     w = torch.empty((B, S, k), dtype=torch.float32, device=normed.device)
     it = torch.empty((B,), dtype=torch.int32, device=normed.device)
