@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--num-corr", type=int, default=1000)
-    ap.add_argument("--pairs", type=int, default=64, help="scan pairs per GPU per step")
+    ap.add_argument("--pairs", type=int, default=128, help="scan pairs per GPU per step")
     ap.add_argument("--preset", default="3dmatch", choices=["3dmatch", "kitti"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
