@@ -294,11 +294,13 @@ enum SplitMode { SPLIT_Q = 0, SPLIT_K = 1, SPLIT_V = 2 };
 // fragment read -- 32 rows, one chunk each -- is conflict-free).  Shared by the
 // Q, K and V products instead of re-splitting per wave and per product.
 constexpr int XS_ROWB = 2 * CH * 2;  // bytes per split row
+template <int PTT>
 PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
-    const int r = tid >> 2;
+    constexpr int TPR = 256 / PTT, CPT = 16 / TPR;  // threads per row, chunks per thread
+    const int r = tid / TPR;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int c = (tid & 3) * 4 + q;
+    for (int q = 0; q < CPT; ++q) {
+        const int c = (tid % TPR) * CPT + q;
         f16x8 hi, lo;
         split8(X + r * xstr + 8 * c, hi, lo);
         const int o = r * XS_ROWB + 16 * (c ^ (r & 15));
@@ -307,15 +309,17 @@ PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
     }
 }
 
-template <int MODE>
+template <int MODE, int NRT>
 PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
                           const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
-    f32x16 acc[2] = {zero16(), zero16()};
+    f32x16 acc[NRT];
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) acc[i] = zero16();
 #pragma unroll
     for (int ks = 0; ks < CH / 16; ++ks) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NRT; ++i) {
             const int r = 32 * i + l32;
             const char *xr = Xs + r * XS_ROWB + 16 * ((2 * ks + h) ^ (r & 15));
             const f16x8 xh = *reinterpret_cast<const f16x8 *>(xr);
@@ -329,7 +333,7 @@ PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, cons
         const int c = ct * 32 + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
         const float bias = pk[off.bias + c];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NRT; ++i) {
             _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * (2 * CH * H3_TILE) + rho * H3_TILE;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -351,7 +355,7 @@ PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, cons
 #pragma unroll
         for (int r = 0; r < 16; ++r) bias[r] = pk[off.bias + ct * 32 + acc_row(r, h)];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NRT; ++i) {
             const int row = p0 + 32 * i + l32;
             _Float16 *drow = dst + (size_t)row * 2 * CH;
 #pragma unroll
@@ -373,21 +377,25 @@ PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, cons
     }
 }
 
-template <int IN, int OUT, int EPI>
+// Y = epi(X W^T + b) over a PTT-point tile (PTT/32 row tiles) by 4 waves.
+template <int IN, int OUT, int EPI, int PTT>
 PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, float *Y,
                       int ystr, const float *__restrict__ resid, int wave, int lane) {
-    constexpr int NCT = OUT / 32;
+    constexpr int NCT = OUT / 32, NRT = PTT / 32;
     if constexpr (NCT >= 4) {
-        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, OUT, EPI, 2>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
-    } else {
+        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, OUT, EPI, NRT>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
+    } else if constexpr (NRT == 2) {
         const int rt = wave & 1, ct = wave >> 1;
         if (ct < NCT) dense_tile<IN, OUT, EPI, 1>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
+    } else {
+        if (wave < NCT) dense_tile<IN, OUT, EPI, 1>(X, xstr, pk, off, 0, wave, Y, ystr, resid, lane);
     }
 }
 
 // Copy a [PT][CH] LDS tile (stride xstr) to global rows [p0, p0 + nrows) (row stride CH).
+template <int PTT>
 PDSC_DEV void store_rows(const float *X, int xstr, float *__restrict__ dst, int p0, int nrows, int tid) {
-    for (int e = tid; e < PT * (CH / 4); e += 256) {
+    for (int e = tid; e < PTT * (CH / 4); e += 256) {
         const int p = e / (CH / 4), c4 = e % (CH / 4);
         if (p < nrows)
             *reinterpret_cast<f32x4 *>(dst + (size_t)(p0 + p) * CH + 4 * c4) =
@@ -405,10 +413,11 @@ struct PwMsg {  // fc_message of one layer
 // LDS: A, B = [PT][S132] (67,584 B -> 2 workgroups per CU).  The fc_message
 // hidden tile C [PT][S68] and pw_first's corr_pos tile live in B, which is free
 // until the residual add writes it.
-constexpr size_t PW_LDS = (size_t)(2 * PT * S132) * sizeof(float);
+template <int PTT> constexpr size_t pw_lds() { return (size_t)(2 * PTT * S132) * sizeof(float); }
 
 // PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> global split layouts); Xout rows -> feat.
 // Q, K, V point at the pair's buffers.
+template <int PTT>
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                       _Float16 *__restrict__ V, int p0, int tid, int wave, int lane) {
@@ -418,22 +427,23 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
     load_wpanel<CH, CH>(pk, d.pcn, wave, lane, ah, al);
     load_wpanel<CH, CH>(pk, d.q, wave, lane, bh, bl);
     asm volatile("" ::: "memory");
-    dense_tile_w<CH, CH, EPI_BN_RELU, 2>(Xin, S132, ah, al, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
+    dense_tile_w<CH, CH, EPI_BN_RELU, PTT / 32>(Xin, S132, ah, al, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
     __syncthreads();  // Xout complete; Xin is dead and now holds the split copy of Xout
     char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
-    split_tile(Xout, S132, Xs, tid);
+    split_tile<PTT>(Xout, S132, Xs, tid);
     load_wpanel<CH, CH>(pk, d.k, wave, lane, ah, al);
     asm volatile("" ::: "memory");
-    store_rows(Xout, S132, feat, p0, PT, tid);
+    store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
     __syncthreads();
-    dense_split<SPLIT_Q>(Xs, bh, bl, pk, d.q, wave, Q, p0, lane);
+    dense_split<SPLIT_Q, PTT / 32>(Xs, bh, bl, pk, d.q, wave, Q, p0, lane);
     load_wpanel<CH, CH>(pk, d.v, wave, lane, bh, bl);
     asm volatile("" ::: "memory");
-    dense_split<SPLIT_K>(Xs, ah, al, pk, d.k, wave, K, p0, lane);
-    dense_split<SPLIT_V>(Xs, bh, bl, pk, d.v, wave, V, p0, lane);
+    dense_split<SPLIT_K, PTT / 32>(Xs, ah, al, pk, d.k, wave, K, p0, lane);
+    dense_split<SPLIT_V, PTT / 32>(Xs, bh, bl, pk, d.v, wave, V, p0, lane);
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
+template <int PTT>
 __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
                                                        size_t l0b, PwDense4 d,
                                                        const float *__restrict__ corr, int in_dim,
@@ -441,11 +451,11 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
                                                        _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                        _Float16 *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *XA = sm, *XB = sm + PT * S132, *cp = XB;  // cp: [PT][in_dim], consumed before XB is written
-    const int b = blockIdx.y, p0 = blockIdx.x * PT;
+    float *XA = sm, *XB = sm + PTT * S132, *cp = XB;  // cp: [PTT][in_dim], consumed before XB is written
+    const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
-    for (int e = tid; e < PT * in_dim; e += 256) {
+    for (int e = tid; e < PTT * in_dim; e += 256) {
         const int p = e / in_dim;
         cp[e] = (p0 + p < N) ? corr[((size_t)b * N + p0) * in_dim + e] : 0.0f;
     }
@@ -456,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
     for (int c = 0; c < IN_MAX; ++c) w[c] = (c < in_dim) ? pk[l0w + j * in_dim + c] : 0.0f;
     const float bj = pk[l0b + j];
     __syncthreads();
-    for (int p = p_off; p < PT; p += 2) {
+    for (int p = p_off; p < PTT; p += 2) {
         float s = 0.0f;
 #pragma unroll
         for (int c = 0; c < IN_MAX; ++c)
@@ -464,16 +474,18 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
         XA[p * S132 + j] = s + bj;
     }
     __syncthreads();
-    pcn_qkv(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    pcn_qkv<PTT>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
+template <int PTT>
 PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restrict__ ml, int b,
                            int nsplit, int Npad, int p0, float *X, int tid) {
-    const int p = tid >> 2;
+    constexpr int TPR = 256 / PTT, NH = 8 / TPR;  // threads per row, 16-channel pieces per thread
+    const int p = tid / TPR;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        const int d0 = (tid & 3) * 32 + half * 16;
+    for (int half = 0; half < NH; ++half) {
+        const int d0 = (tid % TPR) * (16 * NH) + half * 16;
         float out[16];
         combine16(opart, ml, b, nsplit, Npad, p0 + p, d0, out);
 #pragma unroll
@@ -485,16 +497,18 @@ PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restr
 
 // fc_message + residual (:43-44): X = msg (A) -> C -> A (stride S68) -> R (B);
 // C may alias R: it is dead once fc3 has read it (barrier before fc6).
+template <int PTT>
 PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restrict__ pk, const PwMsg &m,
                             const float *__restrict__ feat_rows, int wave, int lane) {
-    dense64<CH, CH2, EPI_BN_RELU>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
+    dense64<CH, CH2, EPI_BN_RELU, PTT>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
     __syncthreads();
-    dense64<CH2, CH2, EPI_BN_RELU>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
+    dense64<CH2, CH2, EPI_BN_RELU, PTT>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
     __syncthreads();
-    dense64<CH2, CH, EPI_RESID>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
+    dense64<CH2, CH, EPI_RESID, PTT>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
     __syncthreads();
 }
 
+template <int PTT>
 __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
@@ -502,55 +516,57 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
                                                      _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                      _Float16 *__restrict__ V) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *XA = sm, *XB = sm + PT * S132, *XC = XB;
-    const int b = blockIdx.y, p0 = blockIdx.x * PT;
+    float *XA = sm, *XB = sm + PTT * S132, *XC = XB;
+    const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
-    combine_tile(opart, ml, b, nsplit, Npad, p0, XA, tid);
+    combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
-    pcn_qkv(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    message_resid<PTT>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    pcn_qkv<PTT>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
+template <int PTT>
 __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
     const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
     const float *__restrict__ feat, float *__restrict__ feat_out, float *__restrict__ normed,
     _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float *XA = sm, *XB = sm + PT * S132, *XC = XB;
-    float *C1 = XA, *C2 = XA + PT * S36;  // classifier hidden layers reuse A
-    const int b = blockIdx.y, p0 = blockIdx.x * PT;
+    float *XA = sm, *XB = sm + PTT * S132, *XC = XB;
+    float *C1 = XA, *C2 = XA + PTT * S36;  // classifier hidden layers reuse A
+    const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
-    const int nrows = min(PT, N - p0);
-    combine_tile(opart, ml, b, nsplit, Npad, p0, XA, tid);
+    const int nrows = min(PTT, N - p0);
+    combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    message_resid<PTT>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     // XB = corr_features rows
-    if (feat_out) store_rows(XB, S132, feat_out + (size_t)b * N * CH, p0, nrows, tid);
-    {   // F.normalize(p=2, dim=-1, eps=1e-12) (:156); 4 lanes per point
-        const int p = tid >> 2, d0 = (tid & 3) * 32;
+    if (feat_out) store_rows<PTT>(XB, S132, feat_out + (size_t)b * N * CH, p0, nrows, tid);
+    {   // F.normalize(p=2, dim=-1, eps=1e-12) (:156); LPP lanes per point
+        constexpr int LPP = 256 / PTT, CPL = CH / LPP;  // lanes per point, channels per lane
+        const int p = tid / LPP, d0 = (tid % LPP) * CPL;
         float ss = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
+        for (int i = 0; i < CPL; ++i) {
             const float x = XB[p * S132 + d0 + i];
             ss = __builtin_fmaf(x, x, ss);
         }
-        ss += __shfl_xor(ss, 1);
-        ss += __shfl_xor(ss, 2);
+#pragma unroll
+        for (int o = 1; o < LPP; o <<= 1) ss += __shfl_xor(ss, o);
         const float den = fmaxf(sqrtf(ss), 1e-12f);
         if (p < nrows) {
             float *dst = normed + ((size_t)b * N + p0 + p) * CH + d0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < CPL / 4; ++i)
                 *reinterpret_cast<f32x4 *>(dst + 4 * i) =
                     f32x4{XB[p * S132 + d0 + 4 * i] / den, XB[p * S132 + d0 + 4 * i + 1] / den,
                           XB[p * S132 + d0 + 4 * i + 2] / den, XB[p * S132 + d0 + 4 * i + 3] / den};
             if (normed_s) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
                 _Float16 *ds = normed_s + ((size_t)b * N + p0 + p) * 2 * CH;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < CPL / 8; ++q) {
                     f16x8 hi, lo;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
@@ -566,9 +582,9 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
         }
     }
     // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171)
-    dense64<CH, CLS, EPI_RELU>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
+    dense64<CH, CLS, EPI_RELU, PTT>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
     __syncthreads();
-    dense64<CLS, CLS, EPI_RELU>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
+    dense64<CLS, CLS, EPI_RELU, PTT>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
     __syncthreads();
     if (tid < nrows) {
         float s = 0.0f;
@@ -580,29 +596,48 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 static PwDense4 dense4(const LayerOff &l) { return PwDense4{l.pcn, l.q, l.k, l.v}; }
 static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
+// Point-tile size: 64 points (two 32-row MFMA tiles per wave, 2 workgroups per
+// CU) once the launch has >= 2 workgroups per CU, else 32 (twice the
+// workgroups for single pairs and small batches).
+static bool small_tiles(int B, int Npad) { return (long)B * (Npad / 64) < 512; }
+
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
                            int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v, hipStream_t s) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pw_first_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed, lay.l0_w,
-                       lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
+    if (small_tiles(B, Npad))
+        hipLaunchKernelGGL(pw_first_kernel<32>, dim3(Npad / 32, B), dim3(256), pw_lds<32>(), s, packed, lay.l0_w,
+                           lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
+    else
+        hipLaunchKernelGGL(pw_first_kernel<64>, dim3(Npad / 64, B), dim3(256), pw_lds<64>(), s, packed, lay.l0_w,
+                           lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
     return hipGetLastError();
 }
 
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, _Float16 *q,
                          _Float16 *k, _Float16 *v, hipStream_t s) {
-    hipLaunchKernelGGL(pw_mid_kernel, dim3(Npad / PT, B), dim3(256), PW_LDS, s, packed,
-                       msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N,
-                       Npad, feat, q, k, v);
+    if (small_tiles(B, Npad))
+        hipLaunchKernelGGL(pw_mid_kernel<32>, dim3(Npad / 32, B), dim3(256), pw_lds<32>(), s, packed,
+                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, q,
+                           k, v);
+    else
+        hipLaunchKernelGGL(pw_mid_kernel<64>, dim3(Npad / 64, B), dim3(256), pw_lds<64>(), s, packed,
+                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, q,
+                           k, v);
     return hipGetLastError();
 }
 
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s) {
-    hipLaunchKernelGGL(pw_last_kernel, dim3((N + PT - 1) / PT, B), dim3(256), PW_LDS, s, packed,
-                       msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml,
-                       nsplit, N, Npad, feat, feat_out, normed, normed_s, conf);
+    if (small_tiles(B, Npad))
+        hipLaunchKernelGGL(pw_last_kernel<32>, dim3((N + 31) / 32, B), dim3(256), pw_lds<32>(), s, packed,
+                           msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N, Npad,
+                           feat, feat_out, normed, normed_s, conf);
+    else
+        hipLaunchKernelGGL(pw_last_kernel<64>, dim3((N + 63) / 64, B), dim3(256), pw_lds<64>(), s, packed,
+                           msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N, Npad,
+                           feat, feat_out, normed, normed_s, conf);
     return hipGetLastError();
 }
 
