@@ -599,7 +599,13 @@ static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 // Point-tile size: 64 points (two 32-row MFMA tiles per wave, 2 workgroups per
 // CU) once the launch has >= 2 workgroups per CU, else 32 (twice the
 // workgroups for single pairs and small batches).
-static bool small_tiles(int B, int Npad) { return (long)B * (Npad / 64) < 512; }
+static bool small_tiles(int B, int Npad) {
+    static const long lim = [] {  // A/B knob (measurement only): PDSC_PW_SMALL_LIMIT
+        const char *e = getenv("PDSC_PW_SMALL_LIMIT");
+        return e ? atol(e) : 512L;
+    }();
+    return (long)B * (Npad / 64) < lim;
+}
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
                            int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v, hipStream_t s) {
