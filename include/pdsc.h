@@ -139,7 +139,8 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
  * d_j = 2 - 2 f_s.f_j, topk(k+1, smallest)[1:] -- the FIRST of the k+1
  * (ascending distance, ascending index) is dropped positionally.
  * Replaces models/common.py:48-69 + models/PointDSC.py:250-252 (only the
- * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k].    */
+ * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k];
+ * 1 <= k <= 63, k + 1 <= N.                                                 */
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S);
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
                       int32_t S, int32_t k, int32_t *knn, void *workspace, size_t workspace_bytes,
@@ -151,7 +152,8 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
  * all S seeds of a pair, as torch.allclose does over the bs*S batch), then
  * w = v / (sum v + 1e-6).  Replaces models/PointDSC.py:257-282, :338-358.
  * sigma_dev / sigma_d_dev: device scalars (learned sigma, sigma_spat).
- * weights [B,S,k]; iters_used [B] int32 (may be NULL).                      */
+ * weights [B,S,k]; iters_used [B] int32 (may be NULL); 1 <= k <= 64.
+ * The workspace holds the fp16 hi/lo split of normed the Gram MFMAs read.    */
 size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t N, int32_t S, int32_t k, int32_t num_iterations);
 int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt,
                          const int32_t *knn, int32_t B, int32_t N, int32_t C, int32_t S, int32_t k,
