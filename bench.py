@@ -385,7 +385,10 @@ def main():
             "metric": "correspondence-pairs/sec through NSM (N=1k/5k) at 1/2/4/8 GPUs; 3DMatch recall parity",
             "value": round(value, 1), "unit": "correspondences/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "dtype_note": "fp32 inputs, outputs and accumulation; the attention, 1x1-conv and kNN/NSM "
+                          "contractions run as 3 fp16 MFMA products (hi*hi + hi*lo + lo*hi) per fp32 product",
+            "data": "synthetic",
             "config": {"workload": f"synthetic random correspondences N={N} ({args.preset}-like, 30% inliers), "
                                    f"{P} scan pairs per GPU per step, full PointDSC testing forward "
                                    f"(12 layers x 128 ch, trained synthetic weights)",
