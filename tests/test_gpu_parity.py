@@ -291,7 +291,7 @@ def test_local_max_bit_exact_random(radius, gpu_device):
         assert np.array_equal(lm[b], O.local_max(src[b], conf[b], radius)), b
 
 
-@pytest.mark.parametrize("N", [300, 2000, 5000])
+@pytest.mark.parametrize("N", [300, 2000, 5000, 9000])  # 9000: rows past the register variants (R = 0)
 def test_seed_knn_random(N, gpu_device):
     """a6 (split-fp16 distances + register radix select) against the oracle's
     fp32 restatement, up to near-ties (assert_knn_equivalent); duplicate rows
