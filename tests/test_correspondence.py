@@ -81,7 +81,7 @@ def _nn_equivalent(ours, ref, dist, axis, eps=2e-6):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("Ns,Nt,D,dups", [(300, 257, 32, 0), (2000, 1500, 33, 0), (5000, 5000, 32, 0),
-                                          (1000, 1200, 32, 40), (64, 1, 16, 0)])
+                                          (1000, 1200, 32, 40), (64, 1, 16, 0), (20000, 18000, 32, 0)])
 def test_mutual_nn_vs_oracle(Ns, Nt, D, dups, gpu_device):
     from pointdsc_amd.correspondence import mutual_nn
     src, tgt, sd, td, gt = _pair(Ns, Nt, D, Ns + Nt, dups=dups)

@@ -50,7 +50,7 @@ def _t(x, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [257, 1000, 5000])
+@pytest.mark.parametrize("N", [257, 1000, 5000, 10001])
 def test_sm_matvec(N, gpu_device):
     from pointdsc_amd.baselines import sm_matvec
     rng = np.random.RandomState(N)
