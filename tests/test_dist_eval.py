@@ -134,3 +134,20 @@ def test_aggregate_scene_then_mean():
     assert abs(out["scene_mean"]["success"] - (2 / 3 + 1) / 2) < 1e-12
     assert abs(out["scene_mean"]["re_deg"] - 4.0) < 1e-12
     assert abs(out["scene_mean"]["te_cm"] - 40.0) < 1e-12
+
+
+@pytest.mark.gpu
+def test_evaluate_synthetic_on_device(gpu_device):
+    """f2 end to end on one GPU: sharded (world 1) synthetic evaluation through
+    forward_batched, per-pair rows and the reference's aggregation."""
+    from pointdsc_amd.PointDSC import PointDSC
+    from pointdsc_amd.synthetic import trained_state_dict
+    m = PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=0.10, sigma_d=0.10, k=40, nms_radius=0.10)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict("3dmatch", 12).items()})
+    m = m.to(gpu_device).eval()
+    stats, summary = ev.evaluate_synthetic(m, 12, 600, "3dmatch", batch=5, device=gpu_device)
+    assert stats.shape == (12, 12)
+    assert summary["pairs"] == 12
+    assert summary["all_pairs"]["success"] >= 0.9  # synthetic pairs with 30 % inliers register
+    assert 0.0 <= summary["all_pairs"]["f1"] <= 1.0
