@@ -37,6 +37,7 @@ CASES = {
     "odd_777":      (12, 777, "3dmatch", 25, 0.2, False, False),
     "rel_5k":       (12, 5000, "3dmatch", 23, 0.3, False, False),
     "rel_5k_lo":    (12, 5000, "3dmatch", 24, 0.06, False, False),  # FPFH-like inlier ratio
+    "rel_5k_kitti": (12, 5000, "kitti", 26, 0.3, False, False),     # BASELINE configs[4] shape
 }
 
 
