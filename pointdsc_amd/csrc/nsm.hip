@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     __shared__ uint32_t fkeyb[4][KNN_FASTCAP];
     __shared__ int fidxb[4][KNN_FASTCAP];
     const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int s = blockIdx.x * 4 + wave;
+    const int s = blockIdx.x * (blockDim.x >> 6) + wave;
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
     const float *row = dist + ((size_t)b * S + s) * N;
     const uint32_t want = k + 1;
@@ -379,25 +379,32 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     }
 }
 
+// Waves (= seeds) per workgroup of the one-wave-per-seed kernels (knn_select,
+// nsm_seed, kabsch_sums; none has a workgroup barrier): 4, unless that leaves
+// fewer than 2 workgroups per CU (a single N = 5000 pair has 500 seeds = 125
+// four-wave workgroups for 256 CUs), then 1 so the seeds spread over all CUs.
+static int seed_wpb(int B, int S) { return (long)B * ((S + 3) / 4) < 512 ? 1 : 4; }
+
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s) {
-    const dim3 grid((S + 3) / 4, B);
+    const int wpb = seed_wpb(B, S);
+    const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const int R = (N + 63) / 64;
     if (R <= 16)
-        hipLaunchKernelGGL(knn_select_kernel<16>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 32)
-        hipLaunchKernelGGL(knn_select_kernel<32>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<32>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 48)
-        hipLaunchKernelGGL(knn_select_kernel<48>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<48>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 64)
-        hipLaunchKernelGGL(knn_select_kernel<64>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<64>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 80)
-        hipLaunchKernelGGL(knn_select_kernel<80>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<80>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 96)
-        hipLaunchKernelGGL(knn_select_kernel<96>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<96>, grid, block, 0, s, dist, N, S, k, knn);
     else if (R <= 128)
-        hipLaunchKernelGGL(knn_select_kernel<128>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<128>, grid, block, 0, s, dist, N, S, k, knn);
     else
-        hipLaunchKernelGGL(knn_select_kernel<0>, grid, dim3(256), 0, s, dist, N, S, k, knn);
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, block, 0, s, dist, N, S, k, knn);
     return hipGetLastError();
 }
 
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restric
                                                        float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
     extern __shared__ __attribute__((aligned(16))) float nsm_sdyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.y, s = blockIdx.x * 4 + wave;
+    const int b = blockIdx.y, s = blockIdx.x * (blockDim.x >> 6) + wave;
     if (s >= S) return;  // wave-uniform
     const int tls = k + 1;
     float *Tl = nsm_sdyn + (size_t)wave * (k * tls + KMAX * NSM_PSTR + KMAX);
@@ -541,13 +548,17 @@ __global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restric
     if (lane == 0) atomicAnd(&pair_mask[b], flags);
 }
 
-size_t nsm_seed_lds_bytes(int k) { return (size_t)4 * (k * (k + 1) + KMAX * NSM_PSTR + KMAX) * sizeof(float); }
+size_t nsm_seed_lds_bytes(int k, int wpb) {
+    return (size_t)wpb * (k * (k + 1) + KMAX * NSM_PSTR + KMAX) * sizeof(float);
+}
 
 hipError_t launch_nsm_seed(const _Float16 *ns, const float *src, const float *tgt, const int *knn, int B, int N,
                            int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
                            unsigned *pair_mask, hipStream_t s) {
     if (k < 1 || k > KMAX) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nsm_seed_kernel, dim3((S + 3) / 4, B), dim3(256), nsm_seed_lds_bytes(k), s, ns, src, tgt, knn,
+    const int wpb = seed_wpb(B, S);
+    hipLaunchKernelGGL(nsm_seed_kernel, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), nsm_seed_lds_bytes(k, wpb), s,
+                       ns, src, tgt, knn,
                        N, S, k, T, sigma, sigma_d, hist, pair_mask);
     return hipGetLastError();
 }
@@ -590,7 +601,7 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
                                                           const float *__restrict__ weights, int N,
                                                           int S, int k, float *__restrict__ sums) {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
-    const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (s >= S) return;
     const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
     float w = 0, ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
@@ -704,7 +715,8 @@ __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restr
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
                              float *sums, hipStream_t s) {
-    hipLaunchKernelGGL(kabsch_sums_kernel, dim3((S + 3) / 4, B), dim3(256), 0, s, src, tgt, knn, weights,
+    const int wpb = seed_wpb(B, S);
+    hipLaunchKernelGGL(kabsch_sums_kernel, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn, weights,
                        N, S, k, sums);
     const int n = B * S;
     hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, seed_trans);
