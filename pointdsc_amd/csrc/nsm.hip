@@ -457,7 +457,7 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
 // independent.
 constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
 
-__global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restrict__ ns,
+__global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const _Float16 *__restrict__ ns,
                                                        const float *__restrict__ src,
                                                        const float *__restrict__ tgt,
                                                        const int *__restrict__ knn, int N, int S, int k, int T,
@@ -482,20 +482,27 @@ __global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restric
         *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{ps[0], ps[1], ps[2], pt[0]};
         *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{pt[1], pt[2], 0.0f, 0.0f};
     }
+    // Gram operands streamed one 16-input k-step at a time (16 VGPRs in
+    // flight instead of both whole 32-row fragments): the wave fits in 128
+    // VGPRs, 4 waves per SIMD to hide the row gathers.  Accumulation order per
+    // tile is unchanged (k-steps ascending).
     const _Float16 *F = ns + (size_t)b * N * 2 * CH;
-    auto load_frag = [&](int t, f16x8 *fh, f16x8 *fl) {
-        const int row = __shfl(idx, 32 * t + l32);
-        const _Float16 *rp = F + (size_t)row * 2 * CH;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            fh[j] = *reinterpret_cast<const f16x8 *>(rp + 8 * (2 * j + h));
-            fl[j] = *reinterpret_cast<const f16x8 *>(rp + CH + 8 * (2 * j + h));
-        }
-    };
-    f16x8 ah[8], al[8], bh[8], bl[8];
     const int nt = (k + 31) / 32;
-    load_frag(0, ah, al);
-    if (nt > 1) load_frag(1, bh, bl);
+    const _Float16 *r0 = F + (size_t)__shfl(idx, l32) * 2 * CH + 8 * h;
+    const _Float16 *r1 = F + (size_t)__shfl(idx, 32 + l32) * 2 * CH + 8 * h;
+    f32x16 G00 = zero16(), G01 = zero16(), G11 = zero16();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const f16x8 ah = *reinterpret_cast<const f16x8 *>(r0 + 16 * j);
+        const f16x8 al = *reinterpret_cast<const f16x8 *>(r0 + CH + 16 * j);
+        G00 = mfma_h3(ah, al, ah, al, G00);
+        if (nt > 1) {
+            const f16x8 bh = *reinterpret_cast<const f16x8 *>(r1 + 16 * j);
+            const f16x8 bl = *reinterpret_cast<const f16x8 *>(r1 + CH + 16 * j);
+            G01 = mfma_h3(ah, al, bh, bl, G01);
+            G11 = mfma_h3(bh, bl, bh, bl, G11);
+        }
+    }
     __builtin_amdgcn_wave_barrier();  // P visible to the wave
     // T for one 32 x 32 Gram tile: rows 32 ta + acc_row(r, h), columns 32 tb + l32
     auto emit = [&](const f32x16 &G, int ta, int tb) {
@@ -527,21 +534,10 @@ __global__ __launch_bounds__(256) void nsm_seed_kernel(const _Float16 *__restric
             Tl[c * tls + a] = val;
         }
     };
-    {
-        f32x16 G = zero16();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) G = mfma_h3(ah[j], al[j], ah[j], al[j], G);
-        emit(G, 0, 0);
-    }
+    emit(G00, 0, 0);
     if (nt > 1) {
-        f32x16 G = zero16();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) G = mfma_h3(ah[j], al[j], bh[j], bl[j], G);
-        emit(G, 0, 1);
-        G = zero16();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) G = mfma_h3(bh[j], bl[j], bh[j], bl[j], G);
-        emit(G, 1, 1);
+        emit(G01, 0, 1);
+        emit(G11, 1, 1);
     }
     __builtin_amdgcn_wave_barrier();
     const unsigned flags = power_iterate(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
