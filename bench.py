@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--path-n", type=int, default=5000, help="N of the compat+NSM path roofline (0 = skip)")
     ap.add_argument("--path-pairs", type=int, default=8)
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="exercise the multi-rank launch/gather plumbing on CPU (gloo), no forward")
     return ap.parse_args()
 
 
@@ -165,11 +167,91 @@ def event_time(fn, iters, stream):
     return start.elapsed_time(end) / iters
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """`bench.py --gpus N` without a launcher around it: start N rank processes
+    of this script (one per GPU, like the reference's mp.spawn in
+    evaluation/test_KITTI.py:220-228), wait for all of them and fail if any
+    fails.  The parent never touches the GPU (no HIP call before the children
+    start, no exec); rank 0's child prints the JSON line."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, WORLD_SIZE=str(args.gpus), RANK=str(r), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    log(f"[launcher] rank {procs.index(p)} exited with {code}; stopping the others")
+                    for q in pending:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def selftest(args, world, rank):
+    """--launcher-selftest: the multi-rank plumbing of the bench without a GPU
+    (gloo on CPU, used by tests/test_bench_launcher.py): strided global pair
+    ids, the all-gather of per-pair result rows, the max-reduce of the timed
+    region and rank 0's single JSON line.  No forward is run, so `value` is null."""
+    import torch.distributed as tdist
+    from pointdsc_amd import dist as pdist
+    from pointdsc_amd.evaluate import pair_stats
+    from pointdsc_amd.synthetic import synthetic_pair
+    if world > 1:
+        tdist.init_process_group("gloo", init_method="env://")
+    n_glob = args.pairs * world
+    mine = pdist.shard_indices(n_glob, rank, world)
+    ps = [synthetic_pair(32, 1000 + g, args.preset) for g in mine]
+    gtT = torch.from_numpy(np.stack([p["gt_trans"] for p in ps]))
+    gtL = torch.from_numpy(np.stack([p["gt_labels"] for p in ps]))
+    rows = torch.cat([pair_stats(gtT, gtT, gtL, gtL), torch.tensor(mine, dtype=torch.float64)[:, None]], 1)
+    t0 = time.perf_counter()
+    if world > 1:
+        tdist.barrier()
+    allrows = pdist.gather_rows(rows, n_glob)
+    _, elapsed = pdist.job_throughput(len(mine), time.perf_counter() - t0)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "value": None, "n_gpus": world, "pairs_total": n_glob,
+                          "pair_ids": allrows[:, -1].long().tolist(),
+                          "synthetic_recall": float(allrows[:, 0].mean()), "elapsed_max_s": elapsed}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and not (args.gpus == 1 and "WORLD_SIZE" not in os.environ):
+        log(f"[rank {rank}] --gpus {args.gpus} but WORLD_SIZE={world}: the process group decides (n_gpus={world})")
+    if args.launcher_selftest:
+        return selftest(args, world, rank)
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -191,7 +273,13 @@ def main():
     model = model.to(dev).eval()
     cfg, packed = model.pdsc_config(), model.packed_weights()
 
-    data = synthetic_batch(P, N, seed=1000 + rank, preset=args.preset)
+    # the job is P pairs per rank; rank r owns the global pairs r, r + W, ... (strided like
+    # DistributedSampler(shuffle=False), evaluation/test_KITTI.py:246-251), pair g seeded by g
+    from pointdsc_amd import dist as pdist
+    from pointdsc_amd.synthetic import synthetic_pair
+    mine = pdist.shard_indices(P * world, rank, world)
+    ps = [synthetic_pair(N, 1000 * 100003 + g, args.preset) for g in mine]
+    data = {k: np.stack([q[k] for q in ps]) for k in ps[0]}
     corr, src, tgt = (torch.from_numpy(data[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
     plan = kernels.ForwardPlan(cfg, packed, P, N, dev)
     stream = torch.cuda.current_stream(dev)
@@ -233,11 +321,13 @@ def main():
     value = world * P * N * args.steps / elapsed
     log(f"[rank {rank}] {ms_per_step:.3f} ms/step -> {value:.4g} correspondences/s")
 
-    # sanity on the last step's output: registrations recover the ground truth
-    T = plan.trans.cpu().numpy()
-    gt = data["gt_trans"]
-    te = np.linalg.norm(T[:, :3, 3] - gt[:, :3, 3], axis=1)
-    recall = float(np.mean(te < 0.3 * (10 if args.preset == "kitti" else 1)))
+    # the last step's per-pair result rows (libs/loss.py metrics, evaluate.pair_stats), gathered
+    # over all ranks with one all_gather (RCCL over xGMI for W > 1): registration recall of the job
+    from pointdsc_amd.evaluate import THRESHOLDS, pair_stats
+    gtT, gtL = torch.from_numpy(data["gt_trans"]).to(dev), torch.from_numpy(data["gt_labels"]).to(dev)
+    rows = pair_stats(plan.trans, gtT, plan.labels, gtL, *THRESHOLDS[args.preset])
+    allrows = pdist.gather_rows(rows, P * world, device=dev)
+    recall = float(allrows[:, 0].mean())
 
     result = None
     if rank == 0:
@@ -246,7 +336,7 @@ def main():
         flops = P * 4.0 * N * N * 128
         achieved = flops / (att_ms * 1e-3) / 1e12
         npad, nsplit = ctypes.c_int32(), ctypes.c_int32()
-        _lib.check(L.pdsc_attention_layout(P, N, ctypes.byref(npad), ctypes.byref(nsplit)), "attention_layout")
+        _lib.check(L.pdsc_attention_layout(P, N, 0, ctypes.byref(npad), ctypes.byref(nsplit)), "attention_layout")
         att_prof = profiled("attention_h3_kernel<4>", P * (npad.value // 128) * nsplit.value * 256)
         roofline = {"kernel": "attention_h3_kernel<4,xcd>", "bound": "mfma",
                     "achieved": round(achieved, 3), "peak": round(PEAK_H3_TFLOPS, 1), "unit": "TFLOP/s",
@@ -395,7 +485,7 @@ def main():
                        "num_corr": N, "pairs_per_gpu_per_step": P, "global_batch": P * world,
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
-            "synthetic_recall": recall,
+            "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
             "stages_ms": stages, "single_pair": single, "cpu_baseline": cpu,

@@ -15,8 +15,10 @@
  *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default
  *     stream), never allocate, never synchronise, and never free caller
  *     memory: scratch comes from a caller-allocated workspace whose size the
- *     matching *_workspace_bytes() query returns.  All functions are
- *     stateless and re-entrant.
+ *     matching *_workspace_bytes() query returns.  The compute functions keep
+ *     no state between calls and may run concurrently on different streams;
+ *     the two measurement hooks (pdsc_attention_timing, pdsc_forward_timing)
+ *     are per-thread settings read by the calls of the thread that set them.
  *   - Return value: PDSC_OK or an error code; no exception crosses the ABI.
  *     pdsc_last_error() returns a thread-local message for the last failure.
  */
@@ -39,6 +41,22 @@ enum pdsc_status {
     PDSC_ERR_UNSUPPORTED = 3, /* valid for the reference, not implemented here */
 };
 
+/* Arithmetic of the fp32 contractions (the reference computes them in fp32).
+ *   PDSC_PRECISION_H3  (default) each fp32 operand is an exact pair hi + lo of
+ *                      fp16 values and each product is hi.hi + hi.lo + lo.hi on
+ *                      the fp16 matrix cores with fp32 accumulation (22-bit
+ *                      operands; 5.3x the fp32 MFMA rate).
+ *   PDSC_PRECISION_F32 exact fp32 MFMA (v_mfma_f32_32x32x2_f32) for the 1x1
+ *                      convolutions, the attention, the seed kNN and the NSM
+ *                      Gram, and libm expf in the softmax: the reference's
+ *                      arithmetic, used to bound the H3 mode's error.
+ * Everything else (M, NMS, power iteration, Kabsch, verification) is the
+ * same code in both modes.                                                   */
+enum pdsc_precision {
+    PDSC_PRECISION_H3 = 0,
+    PDSC_PRECISION_F32 = 1,
+};
+
 /* Hyper-parameters of PointDSC.__init__ (models/PointDSC.py:81-100). */
 typedef struct pdsc_config {
     int32_t in_dim;           /* 6 */
@@ -50,6 +68,7 @@ typedef struct pdsc_config {
     float inlier_threshold;   /* tau of :328/:335 */
     float nms_radius;         /* R of :174 */
     float refine_threshold;   /* :415-418: 0.10 if inlier_threshold == 0.10 else 1.2 */
+    int32_t precision;        /* enum pdsc_precision; the packed weights must be packed with the same value */
 } pdsc_config;
 
 const char *pdsc_version(void);
@@ -57,8 +76,9 @@ const char *pdsc_last_error(void);
 
 /* ---------------------------------------------------------------- weights --
  * Packs the reference's parameters (device pointers, in the order of
- * pdsc_param_names()) into the kernels' layout: Conv1d(k=1) weights re-tiled
- * for 32x32x2 f32 MFMA fragments; eval BatchNorm turned into the per-channel
+ * pdsc_param_names()) into the kernels' layout: Conv1d(k=1) weights as fp16
+ * hi/lo planes scaled by a per-layer power of two (PDSC_PRECISION_H3) or plain
+ * fp32 [out][in] (PDSC_PRECISION_F32); eval BatchNorm turned into the per-channel
  * (alpha, beta) torch-CPU uses (alpha = w / sqrt(var + 1e-5), beta = b - mean*alpha);
  * sigma and sigma_spat copied into the blob header (read on device, no host sync).
  * Replaces: nothing in the reference (it reads nn.Module parameters directly).
@@ -100,16 +120,16 @@ int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const floa
 
 /* The attention core of one NonLocalBlock (models/PointDSC.py:36-42) alone:
  * msg[b,i,:] = sum_j softmax_j(M_ij * q_i.k_j / sqrt(C)) v_j, heads = 1.
- * q,k,v [B,N,C]; msg [B,N,C].  C must be 128.                              */
-size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C);
+ * q,k,v [B,N,C]; msg [B,N,C].  C must be 128.  precision: enum pdsc_precision. */
+size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C, int32_t precision);
 int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const float *M,
-                           int32_t B, int32_t N, int32_t C, float *msg, void *workspace,
+                           int32_t B, int32_t N, int32_t C, int32_t precision, float *msg, void *workspace,
                            size_t workspace_bytes, pdsc_stream_t stream);
 
 /* The encoder's attention geometry for (B, N): padded rows per pair and the
  * number of key splits (partials opart [B,nsplit,Npad,C], ml [B,nsplit,Npad,2]
  * live in the encoder workspace).                                           */
-int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit);
+int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *Npad, int32_t *nsplit);
 
 /* Measurement hook (bench.py): while capacity > 0, every attention launch the
  * encoder issues from the calling thread records start_events[i] / stop_events[i]
@@ -140,11 +160,11 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
  * (ascending distance, ascending index) is dropped positionally.
  * Replaces models/common.py:48-69 + models/PointDSC.py:250-252 (only the
  * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k];
- * 1 <= k <= 63, k + 1 <= N.                                                 */
+ * 1 <= k <= 63, k + 1 <= N.  precision: enum pdsc_precision (distances).   */
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S);
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
-                      int32_t S, int32_t k, int32_t *knn, void *workspace, size_t workspace_bytes,
-                      pdsc_stream_t stream);
+                      int32_t S, int32_t k, int32_t precision, int32_t *knn, void *workspace,
+                      size_t workspace_bytes, pdsc_stream_t stream);
 
 /* ------------------------------------------------ a7-a8 NSM weights --------
  * Local k x k feature x spatial consistency (diag 0), power iteration with
@@ -152,13 +172,14 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
  * all S seeds of a pair, as torch.allclose does over the bs*S batch), then
  * w = v / (sum v + 1e-6).  Replaces models/PointDSC.py:257-282, :338-358.
  * sigma_dev / sigma_d_dev: device scalars (learned sigma, sigma_spat).
- * weights [B,S,k]; iters_used [B] int32 (may be NULL); 1 <= k <= 64.
- * The workspace holds the fp16 hi/lo split of normed the Gram MFMAs read.    */
+ * weights [B,S,k]; iters_used [B] int32 (may be NULL); 1 <= k <= min(63, N-1).
+ * precision: enum pdsc_precision (the feature Gram).  The workspace holds the
+ * fp16 hi/lo split of normed the H3 Gram MFMAs read.                         */
 size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t N, int32_t S, int32_t k, int32_t num_iterations);
 int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt,
                          const int32_t *knn, int32_t B, int32_t N, int32_t C, int32_t S, int32_t k,
-                         int32_t num_iterations, const float *sigma_dev, const float *sigma_d_dev,
-                         float *weights, int32_t *iters_used, void *workspace,
+                         int32_t num_iterations, int32_t precision, const float *sigma_dev,
+                         const float *sigma_d_dev, float *weights, int32_t *iters_used, void *workspace,
                          size_t workspace_bytes, pdsc_stream_t stream);
 
 /* ------------------------------------------------------- a9 Kabsch ---------

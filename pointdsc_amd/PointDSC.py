@@ -71,8 +71,13 @@ class PointDSC(nn.Module):
     """models/PointDSC.py:80-438 with the testing forward on libpdsc."""
 
     def __init__(self, in_dim=6, num_layers=6, num_channels=128, num_iterations=10, ratio=0.1,
-                 inlier_threshold=0.10, sigma_d=0.10, k=40, nms_radius=0.10):
+                 inlier_threshold=0.10, sigma_d=0.10, k=40, nms_radius=0.10, precision="h3"):
+        """The reference's constructor (models/PointDSC.py:81-121) plus ``precision``
+        (not in the reference): 'h3' (default) runs the fp32 contractions as three
+        fp16 MFMA products, 'f32' on exact fp32 MFMA (include/pdsc.h)."""
         super().__init__()
+        _lib.precision_code(precision)
+        self.precision = precision
         self.in_dim = in_dim
         self.num_layers = num_layers
         self.num_iterations = num_iterations
@@ -103,13 +108,13 @@ class PointDSC(nn.Module):
         """Hyper-parameters as the C ABI's ``pdsc_config`` (read at call time,
         so attribute edits after construction are honoured like the reference)."""
         return _lib.make_config(self.in_dim, self.num_layers, self.num_channels, self.num_iterations,
-                                self.k, self.ratio, self.inlier_threshold, self.nms_radius)
+                                self.k, self.ratio, self.inlier_threshold, self.nms_radius, self.precision)
 
     def packed_weights(self) -> torch.Tensor:
         """Kernel-layout weights, re-packed whenever a parameter/buffer changes."""
         named = dict(self.named_parameters())
         named.update(dict(self.named_buffers()))
-        key = tuple((n, t.data_ptr(), t._version) for n, t in sorted(named.items()))
+        key = (self.precision,) + tuple((n, t.data_ptr(), t._version) for n, t in sorted(named.items()))
         if self._packed is None or self._packed_key != key:
             self._packed = kernels.pack_weights(self.pdsc_config(), named)
             self._packed_key = key

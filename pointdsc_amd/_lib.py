@@ -29,7 +29,19 @@ class PdscConfig(ctypes.Structure):
         ("inlier_threshold", c_float),
         ("nms_radius", c_float),
         ("refine_threshold", c_float),
+        ("precision", c_int32),
     ]
+
+
+# enum pdsc_precision (include/pdsc.h)
+PRECISIONS = {"h3": 0, "f32": 1}
+
+
+def precision_code(precision) -> int:
+    """'h3' (default: 3 fp16 MFMA products per fp32 product) or 'f32' (exact fp32 MFMA)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
+    return PRECISIONS[precision]
 
 
 CFG = ctypes.POINTER(PdscConfig)
@@ -47,16 +59,18 @@ _PROTOS = {
     "pdsc_compat_packed_f32": (c_int32, [vp, vp, c_int32, c_int32, vp, vp, vp]),
     "pdsc_encoder_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_encoder_f32": (c_int32, [CFG, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, c_size_t, vp]),
-    "pdsc_attention_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
-    "pdsc_attention_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
-    "pdsc_attention_layout": (c_int32, [c_int32, c_int32, ctypes.POINTER(c_int32), ctypes.POINTER(c_int32)]),
+    "pdsc_attention_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
+    "pdsc_attention_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
+    "pdsc_attention_layout": (c_int32, [c_int32, c_int32, c_int32, ctypes.POINTER(c_int32),
+                                        ctypes.POINTER(c_int32)]),
     "pdsc_attention_timing": (c_int32, [ctypes.POINTER(vp), ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_forward_timing": (c_int32, [ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
     "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
-    "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
+    "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t,
+                                vp]),
     "pdsc_nsm_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32, c_int32]),
-    "pdsc_nsm_weights": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
+    "pdsc_nsm_weights": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32,
                                    vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_rigid_transform_3d": (c_int32, [vp, vp, vp, c_int32, c_int32, vp, vp]),
     "pdsc_seed_hypotheses_workspace_bytes": (c_size_t, [c_int32, c_int32]),
@@ -112,8 +126,9 @@ def check(status: int, what: str):
 
 
 def make_config(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, k=40, ratio=0.1,
-                inlier_threshold=0.10, nms_radius=0.10) -> PdscConfig:
+                inlier_threshold=0.10, nms_radius=0.10, precision="h3") -> PdscConfig:
     """Build ``pdsc_config``; the refine threshold follows models/PointDSC.py:415-418."""
     refine = 0.10 if inlier_threshold == 0.10 else 1.2
     return PdscConfig(int(in_dim), int(num_layers), int(num_channels), int(num_iterations), int(k),
-                      float(ratio), float(inlier_threshold), float(nms_radius), float(refine))
+                      float(ratio), float(inlier_threshold), float(nms_radius), float(refine),
+                      precision_code(precision))

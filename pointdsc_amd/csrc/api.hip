@@ -75,11 +75,14 @@ int check_cfg(const pdsc_config *cfg) {
     if (cfg->num_iterations < 0 || cfg->num_iterations > 31)
         return fail(PDSC_ERR_UNSUPPORTED, "num_iterations=%d not in [0, 31]", cfg->num_iterations);
     if (cfg->k < 1) return fail(PDSC_ERR_ARG, "k=%d", cfg->k);
+    if (cfg->precision != PDSC_PRECISION_H3 && cfg->precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision=%d (PDSC_PRECISION_H3 or PDSC_PRECISION_F32)", cfg->precision);
     return PDSC_OK;
 }
 
 struct Dims {
     int B, N, Npad, S, k, T, nsplit;
+    bool f32;  // PDSC_PRECISION_F32
 };
 
 int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
@@ -91,7 +94,8 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     d.S = (int)((double)N * cfg->ratio);  // int(num_corr * self.ratio) (:174)
     d.k = std::min(cfg->k, N - 1);        // (:250)
     d.T = cfg->num_iterations;
-    d.nsplit = attention_nsplit(B, N);
+    d.f32 = cfg->precision == PDSC_PRECISION_F32;
+    d.nsplit = attention_nsplit(B, N, d.f32);
     if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
     if (d.k > 63) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 63", d.k);
     return PDSC_OK;
@@ -99,7 +103,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
 
 struct EncBufs {
     float *feat, *opart, *ml;
-    _Float16 *q, *k, *v;  // attention_h3 split layouts (hi + lo per element)
+    _Float16 *q, *k, *v;  // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
 };
 
 EncBufs carve_encoder(Carve &c, const Dims &d) {
@@ -117,18 +121,18 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
                 bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s) {
-    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
+    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
-        HIPCHK(launch_attention(e.q, e.k, e.v, M, m_packed, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        HIPCHK(launch_attention(e.q, e.k, e.v, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         if (l + 1 < lay.L)
-            HIPCHK(launch_pw_mid(packed, lay, l, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
+            HIPCHK(launch_pw_mid(packed, lay, l, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
                                  e.k, e.v, s));
         else
-            HIPCHK(launch_pw_last(packed, lay, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
-                                  feat_out, normed, normed_s, conf, s));
+            HIPCHK(launch_pw_last(packed, lay, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
+                                  feat_out, normed, d.f32 ? nullptr : normed_s, conf, s));
     }
     return PDSC_OK;
 }
@@ -148,17 +152,19 @@ NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
     return n;
 }
 
-// normed_s: the split normed copy, or NULL to build it here from normed
-int run_nsm(const float *normed, const _Float16 *normed_s, const float *src, const float *tgt, const int *knn,
-            int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d, const NsmBufs &nb,
-            float *weights, int *iters, hipStream_t s) {
+// normed_s: the split normed copy, or NULL to build it here from normed (H3);
+// f32: the Gram reads normed itself
+int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float *src, const float *tgt,
+            const int *knn, int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d,
+            const NsmBufs &nb, float *weights, int *iters, hipStream_t s) {
     HIPCHK(hipMemsetAsync(nb.mask, 0xff, sizeof(unsigned) * B, s));
-    if (!normed_s) {
+    if (!f32 && !normed_s) {
         HIPCHK(launch_split_rows(normed, (size_t)B * N, nb.ns, s));
         normed_s = nb.ns;
     }
+    const void *feats = f32 ? static_cast<const void *>(normed) : static_cast<const void *>(normed_s);
     if (T > 0)
-        HIPCHK(launch_nsm_seed(normed_s, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
+        HIPCHK(launch_nsm_seed(feats, f32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
     HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, weights, iters, s));
     return PDSC_OK;
 }
@@ -274,10 +280,11 @@ int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *P, float *
     HIPCHK(hipMemsetAsync(packed, 0, lay.total * sizeof(float), s));
     HIPCHK(launch_copy(P[0], packed + lay.sigma, 1, s));
     HIPCHK(launch_copy(P[1], packed + lay.sigma_d, 1, s));
+    const bool f32 = cfg->precision == PDSC_PRECISION_F32;
     auto dense = [&](const DenseOff &o, int wi, int in, int out, bool has_bn) -> hipError_t {
         return launch_pack_dense(P[wi], P[wi + 1], has_bn ? P[wi + 2] : nullptr,
                                  has_bn ? P[wi + 3] : nullptr, has_bn ? P[wi + 4] : nullptr,
-                                 has_bn ? P[wi + 5] : nullptr, in, out, packed + o.w, packed + o.bias,
+                                 has_bn ? P[wi + 5] : nullptr, in, out, f32, packed + o.w, packed + o.bias,
                                  packed + o.alpha, packed + o.beta, packed + o.scale, s);
     };
     for (int l = 0; l < cfg->num_layers; ++l) {
@@ -343,9 +350,9 @@ int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const floa
     return run_encoder(lay, packed, corr_pos, M, false, d, e, feat, normed, nullptr, conf, S_(stream));
 }
 
-size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
-    if (C != CH || B < 1 || N < 1) return 0;
-    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
+size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C, int32_t precision) {
+    if (C != CH || B < 1 || N < 1 || (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)) return 0;
+    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N, precision == PDSC_PRECISION_F32);
     Carve c(nullptr);
     for (int i = 0; i < 3; ++i) c.take<_Float16>((size_t)2 * B * Npad * CH);
     c.take<float>((size_t)B * Npad * CH * ns);
@@ -354,23 +361,31 @@ size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C) {
 }
 
 int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const float *M, int32_t B,
-                           int32_t N, int32_t C, float *msg, void *ws, size_t ws_bytes,
+                           int32_t N, int32_t C, int32_t precision, float *msg, void *ws, size_t ws_bytes,
                            pdsc_stream_t stream) {
     if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
     if (!q || !k || !v || !M || !msg || !ws) return fail(PDSC_ERR_ARG, "null pointer");
     if (B < 1 || N < 1 || N > 32767) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
-    RET_IF(need_ws(ws_bytes, pdsc_attention_workspace_bytes(B, N, C)));
+    if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision=%d", precision);
+    RET_IF(need_ws(ws_bytes, pdsc_attention_workspace_bytes(B, N, C, precision)));
     hipStream_t s = S_(stream);
-    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N);
+    const bool f32 = precision == PDSC_PRECISION_F32;
+    const int Npad = round_up(N, QB), ns = attention_nsplit(B, N, f32);
     Carve c(ws);
     _Float16 *qs = c.take<_Float16>((size_t)2 * B * Npad * CH);
     _Float16 *ks = c.take<_Float16>((size_t)2 * B * Npad * CH);
     _Float16 *vs = c.take<_Float16>((size_t)2 * B * Npad * CH);
     float *op = c.take<float>((size_t)B * Npad * CH * ns);
     float *ml = c.take<float>((size_t)B * Npad * ns * 2);
-    // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
-    HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, s));
-    HIPCHK(launch_attention(qs, ks, vs, M, false, B, N, Npad, ns, op, ml, s));
+    if (f32) {  // the caller's rows, zero-padded to Npad rows (the same bytes as the split layouts)
+        HIPCHK(launch_pad_rows(q, B, N, Npad, reinterpret_cast<float *>(qs), s));
+        HIPCHK(launch_pad_rows(k, B, N, Npad, reinterpret_cast<float *>(ks), s));
+        HIPCHK(launch_pad_rows(v, B, N, Npad, reinterpret_cast<float *>(vs), s));
+    } else {  // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
+        HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, s));
+    }
+    HIPCHK(launch_attention(qs, ks, vs, M, false, f32, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
@@ -394,10 +409,10 @@ int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *coun
     return PDSC_OK;
 }
 
-int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t *Npad, int32_t *nsplit) {
+int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *Npad, int32_t *nsplit) {
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
-    *nsplit = attention_nsplit(B, N);
+    *nsplit = attention_nsplit(B, N, precision == PDSC_PRECISION_F32);
     return PDSC_OK;
 }
 
@@ -418,8 +433,10 @@ size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S) {
 }
 
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
-                      int32_t S, int32_t k, int32_t *knn, void *ws, size_t ws_bytes,
+                      int32_t S, int32_t k, int32_t precision, int32_t *knn, void *ws, size_t ws_bytes,
                       pdsc_stream_t stream) {
+    if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision=%d", precision);
     if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
     if (!normed || !seeds || !knn || !ws) return fail(PDSC_ERR_ARG, "null pointer");
     if (B < 1 || S < 1 || k < 1 || k + 1 > N || k > 63) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
@@ -428,8 +445,12 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
     Carve c(ws);
     float *dist = c.take<float>((size_t)B * S * N);
     _Float16 *ns = c.take<_Float16>((size_t)B * N * 2 * CH);
-    HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
-    HIPCHK(launch_knn_dist(ns, seeds, B, N, S, dist, s));
+    if (precision == PDSC_PRECISION_F32) {
+        HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s));
+    } else {
+        HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
+        HIPCHK(launch_knn_dist(ns, seeds, B, N, S, dist, s));
+    }
     HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
     return PDSC_OK;
 }
@@ -442,17 +463,21 @@ size_t pdsc_nsm_workspace_bytes(int32_t B, int32_t N, int32_t S, int32_t k, int3
 }
 
 int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt, const int32_t *knn,
-                         int32_t B, int32_t N, int32_t C, int32_t S, int32_t k, int32_t T,
+                         int32_t B, int32_t N, int32_t C, int32_t S, int32_t k, int32_t T, int32_t precision,
                          const float *sigma, const float *sigma_d, float *weights, int32_t *iters,
                          void *ws, size_t ws_bytes, pdsc_stream_t stream) {
     if (C != CH) return fail(PDSC_ERR_UNSUPPORTED, "C=%d (only %d)", C, CH);
     if (!normed || !src || !tgt || !knn || !sigma || !sigma_d || !weights || !ws)
         return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || S < 1 || k < 1 || k > 64 || T < 0 || T > 31) return fail(PDSC_ERR_ARG, "B=%d S=%d k=%d T=%d", B, S, k, T);
+    if (B < 1 || S < 1 || k < 1 || k > 63 || N < k + 1 || T < 0 || T > 31)
+        return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d T=%d (1 <= k <= min(63, N-1), 0 <= T <= 31)", B, N, S, k, T);
+    if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision=%d", precision);
     RET_IF(need_ws(ws_bytes, pdsc_nsm_workspace_bytes(B, N, S, k, T)));
     Carve c(ws);
     NsmBufs nb = carve_nsm(c, B, N, S, k, T, true);
-    return run_nsm(normed, nullptr, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb, weights, iters, S_(stream));
+    return run_nsm(normed, nullptr, precision == PDSC_PRECISION_F32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d,
+                   nb, weights, iters, S_(stream));
 }
 
 // -------------------------------------------------------------------- a9
@@ -475,7 +500,8 @@ int32_t pdsc_seed_hypotheses(const float *src, const float *tgt, const int32_t *
                              size_t ws_bytes, pdsc_stream_t stream) {
     if (!src || !tgt || !knn || !weights || !trans || !labels || !seed_trans)
         return fail(PDSC_ERR_ARG, "null pointer (seed_trans is required as scratch)");
-    if (B < 1 || N < 1 || S < 1 || k < 1 || k > 64) return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d", B, N, S, k);
+    if (B < 1 || S < 1 || k < 1 || k > 63 || N < k + 1)
+        return fail(PDSC_ERR_ARG, "B=%d N=%d S=%d k=%d (1 <= k <= min(63, N-1))", B, N, S, k);
     hipStream_t s = S_(stream);
     // the integer inlier counts live in the caller's fitness buffer until select_best turns
     // each into count / N (same thread, same element)
@@ -529,7 +555,7 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     if (ev) HIPCHK(hipEventRecord(ev[i], s))
     STAGE(0);
     // a1 (:150-153)
-    const bool mpacked = !dense_m_requested();
+    const bool mpacked = !dense_m_requested() && !d.f32;  // the exact-fp32 attention reads dense M
     if (mpacked)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
     else
@@ -544,11 +570,14 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     STAGE(3);
     // a6 (:250-252)
     HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
-    HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    if (d.f32)
+        HIPCHK(launch_knn_dist_f32(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    else
+        HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
     HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
     STAGE(4);
     // a7-a8 (:257-282)
-    RET_IF(run_nsm(f.normed, f.normed_s, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
+    RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
                    nullptr, s));
     STAGE(5);
     // a9-a10 (:287-335)

@@ -24,6 +24,7 @@
 // split-K over keys when B*N is too small to fill 256 CUs.
 #include <cstdlib>
 
+#include "attention.hpp"
 #include "attention_h3.hpp"
 
 namespace pdsc {
@@ -31,8 +32,13 @@ namespace pdsc {
 // ============================================================ weight packing
 // Per-layer power-of-two scale: max|W| 2^s <= 2^14 keeps hi and (for all but
 // the weights 2^-17 below the layer's largest) lo in fp16's normal range.
-__global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w, int n, float *__restrict__ sc) {
+__global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w, int n, int f32,
+                                                     float *__restrict__ sc) {
     __shared__ float part[4];
+    if (f32) {  // exact-fp32 weights are stored unscaled
+        if (threadIdx.x == 0) sc[0] = sc[1] = 1.0f;
+        return;
+    }
     float m = 0.0f;
     for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
     m = wave_max(m);
@@ -50,16 +56,19 @@ __global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w
 
 // W [out][in] (torch Conv1d weight) -> hi / lo fp16 planes of W * 2^s, same
 // [out][in] order: lane (h, n) of a 32x32x16 MFMA reads 8 consecutive inputs of
-// output n as one 16-B load.  BN folded as torch-CPU eval folds it.
+// output n as one 16-B load (f32: W itself, fp32 [out][in]).  BN folded as
+// torch-CPU eval folds it.
 __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__restrict__ b,
                                   const float *__restrict__ bn_w, const float *__restrict__ bn_b,
                                   const float *__restrict__ bn_rm, const float *__restrict__ bn_rv,
-                                  int in, int out, float *__restrict__ dw, float *__restrict__ db,
+                                  int in, int out, int f32, float *__restrict__ dw, float *__restrict__ db,
                                   float *__restrict__ da, float *__restrict__ dbeta,
                                   const float *__restrict__ sc) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = in * out;
-    if (i < total) {
+    if (i < total && f32) {
+        dw[i] = w[i];
+    } else if (i < total) {
         _Float16 *wh = reinterpret_cast<_Float16 *>(dw), *wl = wh + total;
         _Float16 hi, lo;
         split_h(w[i] * sc[1], hi, lo);
@@ -87,12 +96,12 @@ __global__ void copy_kernel(const float *__restrict__ s, float *__restrict__ d, 
 }
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
-                             const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
+                             const float *bn_rm, const float *bn_rv, int in, int out, bool f32, float *dst_w,
                              float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s) {
     const int n = in * out;
-    hipLaunchKernelGGL(wscale_kernel, dim3(1), dim3(256), 0, s, w, n, dst_scale);
+    hipLaunchKernelGGL(wscale_kernel, dim3(1), dim3(256), 0, s, w, n, (int)f32, dst_scale);
     hipLaunchKernelGGL(pack_dense_kernel, dim3((n + 255) / 256), dim3(256), 0, s, w, b, bn_w, bn_b,
-                       bn_rm, bn_rv, in, out, dst_w, dst_b, dst_a, dst_beta, dst_scale);
+                       bn_rm, bn_rv, in, out, (int)f32, dst_w, dst_b, dst_a, dst_beta, dst_scale);
     return hipGetLastError();
 }
 
@@ -119,12 +128,27 @@ static int att_target() {
     return t;
 }
 static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, N, att_target()); }
+// PDSC_PRECISION_F32: attention.hpp's exact-fp32 MFMA kernel, 32-key stages, libm expf
+constexpr int ATT_F32_KTS = 32;
+static AttnGrid f32_grid(int B, int N) { return attention_grid<ATT_NW, ATT_F32_KTS>(B, N, att_target()); }
 
-int attention_nsplit(int B, int N) { return prod_grid(B, N).nsplit; }
+int attention_nsplit(int B, int N, bool f32) { return f32 ? f32_grid(B, N).nsplit : prod_grid(B, N).nsplit; }
 
-hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
-                            bool m_packed, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+hipError_t launch_attention(const void *q, const void *k, const void *v, const float *M, bool m_packed,
+                            bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s) {
+    if (f32) {  // fp32 [B][Npad][CH] rows, dense M
+        const AttnGrid g = f32_grid(B, N);
+        if (m_packed || g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
+        const size_t lds = attention_lds_bytes<ATT_NW, ATT_F32_KTS>();
+        hipLaunchKernelGGL((attention_kernel_t<ATT_NW, ATT_F32_KTS, false, true>), dim3(g.B * g.nqb * g.nsplit),
+                           dim3(ATT_NW * 64), lds, s,
+                           static_cast<const float *>(q), static_cast<const float *>(k),
+                           static_cast<const float *>(v), M, g, opart, ml);
+        return hipGetLastError();
+    }
+    const _Float16 *qs = static_cast<const _Float16 *>(q), *ks = static_cast<const _Float16 *>(k),
+                   *vs = static_cast<const _Float16 *>(v);
     const AttnGridH3 g = prod_grid(B, N);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     if (m_packed)
@@ -133,6 +157,20 @@ hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float
     else
         hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), dim3(g.B * g.nqb * g.nsplit),
                            dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+    return hipGetLastError();
+}
+
+// fp32 rows [B][N][CH] -> [B][Npad][CH] with zero padding rows (the f32 attention's input)
+__global__ void pad_rows_kernel(const float *__restrict__ x, int B, int N, int Npad, float *__restrict__ y) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)B * Npad * CH) return;
+    const int c = (int)(i % CH), row = (int)((i / CH) % Npad), b = (int)(i / CH / Npad);
+    y[i] = row < N ? x[((size_t)b * N + row) * CH + c] : 0.0f;
+}
+
+hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s) {
+    const size_t n = (size_t)B * Npad * CH;
+    hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, B, N, Npad, y);
     return hipGetLastError();
 }
 
@@ -199,18 +237,35 @@ enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
 constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
 constexpr int IN_MAX = 16;  // layer0 input width held in registers
 
-// The wave's weight panel for output tile ct: per 16-input k-step, the hi and
-// lo fragments (lane (h, n): inputs 16 ks + 8h .. +7 of output 32 ct + n).
-template <int IN, int OUT>
-PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int ct, int lane, f16x8 *wh,
-                          f16x8 *wl) {
-    const _Float16 *Wh = reinterpret_cast<const _Float16 *>(pk + off.w);
-    const _Float16 *Wl = Wh + (size_t)OUT * IN;
-    const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 8 * (lane >> 5);
+// The wave's weight panel for output tile ct.  H3: per 16-input k-step, the hi
+// and lo fragments (lane (h, n): inputs 16 ks + 8h .. +7 of output 32 ct + n).
+// F32: per 8-input chunk j, lane (h, n) holds inputs 8j + 4h .. +3 of output
+// 32 ct + n -- the exact-fp32 MFMA's k-step 4j + e uses input 8j + 4h + e (the
+// activations are read with the same map, so the products pair up).
+template <int IN, bool F32> struct WPanel;
+template <int IN> struct WPanel<IN, false> {
+    f16x8 h[IN / 16], l[IN / 16];
+};
+template <int IN> struct WPanel<IN, true> {
+    f32x4 w[IN / 8];
+};
+
+template <int IN, int OUT, bool F32>
+PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int ct, int lane, WPanel<IN, F32> &p) {
+    if constexpr (F32) {
+        const float *W = pk + off.w;
+        const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 4 * (lane >> 5);
 #pragma unroll
-    for (int ks = 0; ks < IN / 16; ++ks) {
-        wh[ks] = *reinterpret_cast<const f16x8 *>(Wh + rowo + 16 * ks);
-        wl[ks] = *reinterpret_cast<const f16x8 *>(Wl + rowo + 16 * ks);
+        for (int j = 0; j < IN / 8; ++j) p.w[j] = *reinterpret_cast<const f32x4 *>(W + rowo + 8 * j);
+    } else {
+        const _Float16 *Wh = reinterpret_cast<const _Float16 *>(pk + off.w);
+        const _Float16 *Wl = Wh + (size_t)OUT * IN;
+        const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 8 * (lane >> 5);
+#pragma unroll
+        for (int ks = 0; ks < IN / 16; ++ks) {
+            p.h[ks] = *reinterpret_cast<const f16x8 *>(Wh + rowo + 16 * ks);
+            p.l[ks] = *reinterpret_cast<const f16x8 *>(Wl + rowo + 16 * ks);
+        }
     }
 }
 
@@ -229,26 +284,40 @@ PDSC_DEV void split8(const float *x, f16x8 &hi, f16x8 &lo) {
     }
 }
 
-// One 32-output tile of Y = epi(X W^T + b) for NRT row tiles, on the fp16
-// matrix cores with the 3-product split (attention_h3.hpp): activations split
+// One 32-output tile of Y = epi(X W^T + b) for NRT row tiles.  H3: the fp16
+// matrix cores with the 3-product split (attention_h3.hpp), activations split
 // as they are read from LDS, weights pre-split and pre-scaled by 2^s (the
-// accumulator is scaled back by the exact 2^-s before the bias).
-template <int IN, int OUT, int EPI, int NRT>
-PDSC_DEV void dense_tile_w(const float *X, int xstr, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
+// accumulator is scaled back by the exact 2^-s before the bias).  F32: exact
+// fp32 MFMA 32x32x2 on the fp32 activations and weights.
+template <int IN, int OUT, int EPI, int NRT, bool F32>
+PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, const float *__restrict__ pk,
                            const DenseOff &off, int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid,
                            int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
 #pragma unroll
     for (int i = 0; i < NRT; ++i) acc[i] = zero16();
-    const float *xp = X + (rt0 * 32 + l32) * xstr + 8 * h;
+    if constexpr (F32) {
+        const float *xp = X + (rt0 * 32 + l32) * xstr + 4 * h;
 #pragma unroll
-    for (int ks = 0; ks < IN / 16; ++ks) {
+        for (int j = 0; j < IN / 8; ++j) {
 #pragma unroll
-        for (int i = 0; i < NRT; ++i) {
-            f16x8 xh, xl;
-            split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
-            acc[i] = mfma_h3(xh, xl, wh[ks], wl[ks], acc[i]);
+            for (int i = 0; i < NRT; ++i) {
+                const f32x4 xv = *reinterpret_cast<const f32x4 *>(xp + i * 32 * xstr + 8 * j);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i] = mfma32(xv[e], wp.w[j][e], acc[i]);
+            }
+        }
+    } else {
+        const float *xp = X + (rt0 * 32 + l32) * xstr + 8 * h;
+#pragma unroll
+        for (int ks = 0; ks < IN / 16; ++ks) {
+#pragma unroll
+            for (int i = 0; i < NRT; ++i) {
+                f16x8 xh, xl;
+                split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
+                acc[i] = mfma_h3(xh, xl, wp.h[ks], wp.l[ks], acc[i]);
+            }
         }
     }
     const int j = ct * 32 + l32;
@@ -268,15 +337,15 @@ PDSC_DEV void dense_tile_w(const float *X, int xstr, const f16x8 *wh, const f16x
         }
 }
 
-template <int IN, int OUT, int EPI, int NRT>
+template <int IN, int OUT, int EPI, int NRT, bool F32>
 PDSC_DEV void dense_tile(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off,
                          int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid, int lane) {
-    f16x8 wh[IN / 16], wl[IN / 16];  // the wave's whole weight panel, issued up front
-    load_wpanel<IN, OUT>(pk, off, ct, lane, wh, wl);
+    WPanel<IN, F32> wp;  // the wave's whole weight panel, issued up front
+    load_wpanel<IN, OUT, F32>(pk, off, ct, lane, wp);
     // keep the scheduler from sinking the loads next to their uses (each would
     // then expose a full L2 round trip per k-step); waits stay counted
     asm volatile("" ::: "memory");
-    dense_tile_w<IN, OUT, EPI, NRT>(X, xstr, wh, wl, pk, off, rt0, ct, Y, ystr, resid, lane);
+    dense_tile_w<IN, OUT, EPI, NRT, F32>(X, xstr, wp, pk, off, rt0, ct, Y, ystr, resid, lane);
 }
 
 // Q/K/V projections (Conv1d 128 -> 128 + bias, :36-38) of the PT-point tile,
@@ -310,7 +379,7 @@ PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
 }
 
 template <int MODE, int NRT>
-PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, const float *__restrict__ pk,
+PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const float *__restrict__ pk,
                           const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
@@ -324,8 +393,8 @@ PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, cons
             const char *xr = Xs + r * XS_ROWB + 16 * ((2 * ks + h) ^ (r & 15));
             const f16x8 xh = *reinterpret_cast<const f16x8 *>(xr);
             const f16x8 xl = *reinterpret_cast<const f16x8 *>(xr + CH * 2);
-            acc[i] = MODE == SPLIT_V ? mfma_h3(xh, xl, wh[ks], wl[ks], acc[i])
-                                     : mfma_h3(wh[ks], wl[ks], xh, xl, acc[i]);
+            acc[i] = MODE == SPLIT_V ? mfma_h3(xh, xl, wp.h[ks], wp.l[ks], acc[i])
+                                     : mfma_h3(wp.h[ks], wp.l[ks], xh, xl, acc[i]);
         }
     }
     const float inv = pk[off.scale];
@@ -378,17 +447,18 @@ PDSC_DEV void dense_split(const char *Xs, const f16x8 *wh, const f16x8 *wl, cons
 }
 
 // Y = epi(X W^T + b) over a PTT-point tile (PTT/32 row tiles) by 4 waves.
-template <int IN, int OUT, int EPI, int PTT>
+template <int IN, int OUT, int EPI, int PTT, bool F32>
 PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, float *Y,
                       int ystr, const float *__restrict__ resid, int wave, int lane) {
     constexpr int NCT = OUT / 32, NRT = PTT / 32;
     if constexpr (NCT >= 4) {
-        for (int ct = wave; ct < NCT; ct += 4) dense_tile<IN, OUT, EPI, NRT>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
+        for (int ct = wave; ct < NCT; ct += 4)
+            dense_tile<IN, OUT, EPI, NRT, F32>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
     } else if constexpr (NRT == 2) {
         const int rt = wave & 1, ct = wave >> 1;
-        if (ct < NCT) dense_tile<IN, OUT, EPI, 1>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
+        if (ct < NCT) dense_tile<IN, OUT, EPI, 1, F32>(X, xstr, pk, off, rt, ct, Y, ystr, resid, lane);
     } else {
-        if (wave < NCT) dense_tile<IN, OUT, EPI, 1>(X, xstr, pk, off, 0, wave, Y, ystr, resid, lane);
+        if (wave < NCT) dense_tile<IN, OUT, EPI, 1, F32>(X, xstr, pk, off, 0, wave, Y, ystr, resid, lane);
     }
 }
 
@@ -415,35 +485,49 @@ struct PwMsg {  // fc_message of one layer
 // until the residual add writes it.
 template <int PTT> constexpr size_t pw_lds() { return (size_t)(2 * PTT * S132) * sizeof(float); }
 
-// PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> global split layouts); Xout rows -> feat.
-// Q, K, V point at the pair's buffers.
-template <int PTT>
+// PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> the attention's input layouts);
+// Xout rows -> feat.  Q, K, V point at the pair's buffers: the fp16 hi/lo split
+// layouts (H3) or fp32 [Npad][CH] rows (F32, same bytes).
+template <int PTT, bool F32>
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                       _Float16 *__restrict__ V, int p0, int tid, int wave, int lane) {
     // four 128 -> 128 products with the same wave -> output-tile map (ct = wave):
     // each one's weight panel is fetched while the previous one computes
-    f16x8 ah[CH / 16], al[CH / 16], bh[CH / 16], bl[CH / 16];
-    load_wpanel<CH, CH>(pk, d.pcn, wave, lane, ah, al);
-    load_wpanel<CH, CH>(pk, d.q, wave, lane, bh, bl);
+    WPanel<CH, F32> pa, pb;
+    load_wpanel<CH, CH, F32>(pk, d.pcn, wave, lane, pa);
+    load_wpanel<CH, CH, F32>(pk, d.q, wave, lane, pb);
     asm volatile("" ::: "memory");
-    dense_tile_w<CH, CH, EPI_BN_RELU, PTT / 32>(Xin, S132, ah, al, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
-    __syncthreads();  // Xout complete; Xin is dead and now holds the split copy of Xout
-    char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
-    split_tile<PTT>(Xout, S132, Xs, tid);
-    load_wpanel<CH, CH>(pk, d.k, wave, lane, ah, al);
-    asm volatile("" ::: "memory");
-    store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
-    __syncthreads();
-    dense_split<SPLIT_Q, PTT / 32>(Xs, bh, bl, pk, d.q, wave, Q, p0, lane);
-    load_wpanel<CH, CH>(pk, d.v, wave, lane, bh, bl);
-    asm volatile("" ::: "memory");
-    dense_split<SPLIT_K, PTT / 32>(Xs, ah, al, pk, d.k, wave, K, p0, lane);
-    dense_split<SPLIT_V, PTT / 32>(Xs, bh, bl, pk, d.v, wave, V, p0, lane);
+    dense_tile_w<CH, CH, EPI_BN_RELU, PTT / 32, F32>(Xin, S132, pa, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
+    __syncthreads();  // Xout complete; Xin is dead (H3: it now holds the split copy of Xout)
+    if constexpr (F32) {
+        float *Qf = reinterpret_cast<float *>(Q) + (size_t)p0 * CH, *Kf = reinterpret_cast<float *>(K) + (size_t)p0 * CH,
+              *Vf = reinterpret_cast<float *>(V) + (size_t)p0 * CH;
+        load_wpanel<CH, CH, F32>(pk, d.k, wave, lane, pa);
+        asm volatile("" ::: "memory");
+        store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
+        dense_tile_w<CH, CH, EPI_BIAS, PTT / 32, F32>(Xout, S132, pb, pk, d.q, 0, wave, Qf, CH, nullptr, lane);
+        load_wpanel<CH, CH, F32>(pk, d.v, wave, lane, pb);
+        asm volatile("" ::: "memory");
+        dense_tile_w<CH, CH, EPI_BIAS, PTT / 32, F32>(Xout, S132, pa, pk, d.k, 0, wave, Kf, CH, nullptr, lane);
+        dense_tile_w<CH, CH, EPI_BIAS, PTT / 32, F32>(Xout, S132, pb, pk, d.v, 0, wave, Vf, CH, nullptr, lane);
+    } else {
+        char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
+        split_tile<PTT>(Xout, S132, Xs, tid);
+        load_wpanel<CH, CH, F32>(pk, d.k, wave, lane, pa);
+        asm volatile("" ::: "memory");
+        store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
+        __syncthreads();
+        dense_split<SPLIT_Q, PTT / 32>(Xs, pb, pk, d.q, wave, Q, p0, lane);
+        load_wpanel<CH, CH, F32>(pk, d.v, wave, lane, pb);
+        asm volatile("" ::: "memory");
+        dense_split<SPLIT_K, PTT / 32>(Xs, pa, pk, d.k, wave, K, p0, lane);
+        dense_split<SPLIT_V, PTT / 32>(Xs, pb, pk, d.v, wave, V, p0, lane);
+    }
 }
 
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
-template <int PTT>
+template <int PTT, bool F32>
 __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
                                                        size_t l0b, PwDense4 d,
                                                        const float *__restrict__ corr, int in_dim,
@@ -474,7 +558,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
         XA[p * S132 + j] = s + bj;
     }
     __syncthreads();
-    pcn_qkv<PTT>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    pcn_qkv<PTT, F32>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
@@ -497,18 +581,18 @@ PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restr
 
 // fc_message + residual (:43-44): X = msg (A) -> C -> A (stride S68) -> R (B);
 // C may alias R: it is dead once fc3 has read it (barrier before fc6).
-template <int PTT>
+template <int PTT, bool F32>
 PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restrict__ pk, const PwMsg &m,
                             const float *__restrict__ feat_rows, int wave, int lane) {
-    dense64<CH, CH2, EPI_BN_RELU, PTT>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
+    dense64<CH, CH2, EPI_BN_RELU, PTT, F32>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
     __syncthreads();
-    dense64<CH2, CH2, EPI_BN_RELU, PTT>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
+    dense64<CH2, CH2, EPI_BN_RELU, PTT, F32>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
     __syncthreads();
-    dense64<CH2, CH, EPI_RESID, PTT>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
+    dense64<CH2, CH, EPI_RESID, PTT, F32>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
     __syncthreads();
 }
 
-template <int PTT>
+template <int PTT, bool F32>
 __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
@@ -522,11 +606,11 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     const size_t boff = (size_t)b * Npad * CH;
     combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid<PTT>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
-    pcn_qkv<PTT>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
 }
 
-template <int PTT>
+template <int PTT, bool F32>
 __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
     const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
@@ -541,7 +625,7 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const int nrows = min(PTT, N - p0);
     combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
-    message_resid<PTT>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     // XB = corr_features rows
     if (feat_out) store_rows<PTT>(XB, S132, feat_out + (size_t)b * N * CH, p0, nrows, tid);
     {   // F.normalize(p=2, dim=-1, eps=1e-12) (:156); LPP lanes per point
@@ -563,7 +647,7 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
                 *reinterpret_cast<f32x4 *>(dst + 4 * i) =
                     f32x4{XB[p * S132 + d0 + 4 * i] / den, XB[p * S132 + d0 + 4 * i + 1] / den,
                           XB[p * S132 + d0 + 4 * i + 2] / den, XB[p * S132 + d0 + 4 * i + 3] / den};
-            if (normed_s) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
+            if (!F32 && normed_s) {  // the fp16 hi/lo split copy (qk_pos order) the H3 seed kNN consumes
                 _Float16 *ds = normed_s + ((size_t)b * N + p0 + p) * 2 * CH;
 #pragma unroll
                 for (int q = 0; q < CPL / 8; ++q) {
@@ -582,9 +666,9 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
         }
     }
     // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171)
-    dense64<CH, CLS, EPI_RELU, PTT>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
+    dense64<CH, CLS, EPI_RELU, PTT, F32>(XB, S132, pk, c0, C1, S36, nullptr, wave, lane);
     __syncthreads();
-    dense64<CLS, CLS, EPI_RELU, PTT>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
+    dense64<CLS, CLS, EPI_RELU, PTT, F32>(C1, S36, pk, c2, C2, S36, nullptr, wave, lane);
     __syncthreads();
     if (tid < nrows) {
         float s = 0.0f;
@@ -607,44 +691,46 @@ static bool small_tiles(int B, int Npad) {
     return (long)B * (Npad / 64) < lim;
 }
 
-hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
-                           int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v, hipStream_t s) {
+// One launch of pointwise kernel K<PTT, F32> with PTT and F32 picked at run time.
+#define PW_LAUNCH(K, rows, ...)                                                                         \
+    do {                                                                                                \
+        const bool st_ = small_tiles(B, Npad);                                                          \
+        const int pt_ = st_ ? 32 : 64;                                                                  \
+        const dim3 g_(((rows) + pt_ - 1) / pt_, B);                                                     \
+        if (st_ && f32)                                                                                 \
+            hipLaunchKernelGGL((K<32, true>), g_, dim3(256), pw_lds<32>(), s, __VA_ARGS__);             \
+        else if (st_)                                                                                   \
+            hipLaunchKernelGGL((K<32, false>), g_, dim3(256), pw_lds<32>(), s, __VA_ARGS__);            \
+        else if (f32)                                                                                   \
+            hipLaunchKernelGGL((K<64, true>), g_, dim3(256), pw_lds<64>(), s, __VA_ARGS__);             \
+        else                                                                                            \
+            hipLaunchKernelGGL((K<64, false>), g_, dim3(256), pw_lds<64>(), s, __VA_ARGS__);            \
+    } while (0)
+
+hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
+                           int N, int Npad, float *feat, void *q, void *k, void *v, hipStream_t s) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
-    if (small_tiles(B, Npad))
-        hipLaunchKernelGGL(pw_first_kernel<32>, dim3(Npad / 32, B), dim3(256), pw_lds<32>(), s, packed, lay.l0_w,
-                           lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
-    else
-        hipLaunchKernelGGL(pw_first_kernel<64>, dim3(Npad / 64, B), dim3(256), pw_lds<64>(), s, packed, lay.l0_w,
-                           lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, q, k, v);
+    _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
+    PW_LAUNCH(pw_first_kernel, Npad, packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad,
+              feat, Q, K, V);
     return hipGetLastError();
 }
 
-hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, _Float16 *q,
-                         _Float16 *k, _Float16 *v, hipStream_t s) {
-    if (small_tiles(B, Npad))
-        hipLaunchKernelGGL(pw_mid_kernel<32>, dim3(Npad / 32, B), dim3(256), pw_lds<32>(), s, packed,
-                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, q,
-                           k, v);
-    else
-        hipLaunchKernelGGL(pw_mid_kernel<64>, dim3(Npad / 64, B), dim3(256), pw_lds<64>(), s, packed,
-                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, q,
-                           k, v);
+hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
+                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
+                         hipStream_t s) {
+    _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
+    PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,
+              N, Npad, feat, Q, K, V);
     return hipGetLastError();
 }
 
-hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
+hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s) {
-    if (small_tiles(B, Npad))
-        hipLaunchKernelGGL(pw_last_kernel<32>, dim3((N + 31) / 32, B), dim3(256), pw_lds<32>(), s, packed,
-                           msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N, Npad,
-                           feat, feat_out, normed, normed_s, conf);
-    else
-        hipLaunchKernelGGL(pw_last_kernel<64>, dim3((N + 63) / 64, B), dim3(256), pw_lds<64>(), s, packed,
-                           msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N, Npad,
-                           feat, feat_out, normed, normed_s, conf);
+    PW_LAUNCH(pw_last_kernel, N, packed, msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml,
+              nsplit, N, Npad, feat, feat_out, normed, normed_s, conf);
     return hipGetLastError();
 }
-
+#undef PW_LAUNCH
 }  // namespace pdsc

@@ -95,6 +95,55 @@ hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, i
     return hipGetLastError();
 }
 
+// PDSC_PRECISION_F32: the same seed rows of 2 - 2 F F^T on exact fp32 MFMA
+// (32x32x2), straight from the fp32 normed rows [B][N][128].  A wave owns 32
+// seeds (its 64 fp32 fragment values per lane held for the launch) and sweeps
+// KNN_KPB key tiles, each key fragment read from L2 as 16-B pieces; k-step
+// 4j + e of lane (h, .) is channel 8j + 4h + e for both operands.
+__global__ __launch_bounds__(256) void knn_dist_f32_kernel(const float *__restrict__ normed,
+                                                           const int *__restrict__ seeds, int N, int S,
+                                                           float *__restrict__ dist) {
+    const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int s0 = (blockIdx.y * 4 + wave) * 32;
+    if (s0 >= S) return;  // wave-uniform; no barriers
+    const float *F = normed + (size_t)b * N * CH;
+    const int sidx = s0 + l32;
+    const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
+    const float *srow = F + (size_t)min(max(seed, 0), N - 1) * CH + 4 * h;
+    f32x4 a[CH / 8];
+#pragma unroll
+    for (int j = 0; j < CH / 8; ++j) a[j] = *reinterpret_cast<const f32x4 *>(srow + 8 * j);
+    const int nkt = (N + 31) / 32;
+    const int t0 = blockIdx.x * KNN_KPB, t1 = min(t0 + KNN_KPB, nkt);
+    for (int t = t0; t < t1; ++t) {
+        const int j = t * 32 + l32;
+        const float *krow = F + (size_t)min(j, N - 1) * CH + 4 * h;
+        f32x16 acc = zero16();
+#pragma unroll
+        for (int jj = 0; jj < CH / 8; ++jj) {
+            const f32x4 bv = *reinterpret_cast<const f32x4 *>(krow + 8 * jj);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = mfma32(a[jj][e], bv[e], acc);
+        }
+        if (j < N) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int sr = s0 + acc_row(r, h);
+                if (sr < S) dist[((size_t)b * S + sr) * N + j] = 2.0f - 2.0f * acc[r];
+            }
+        }
+    }
+}
+
+hipError_t launch_knn_dist_f32(const float *normed, const int *seeds, int B, int N, int S, float *dist,
+                               hipStream_t s) {
+    const int nkt = (N + 31) / 32;
+    hipLaunchKernelGGL(knn_dist_f32_kernel, dim3((nkt + KNN_KPB - 1) / KNN_KPB, (S + 127) / 128, B), dim3(256), 0,
+                       s, normed, seeds, N, S, dist);
+    return hipGetLastError();
+}
+
 // fp32 rows [rows][128] -> [rows][2][128] fp16 hi/lo in qk_pos order (standalone API)
 __global__ void split_rows_kernel(const float *__restrict__ x, size_t rows, _Float16 *__restrict__ out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -457,7 +506,10 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
 // independent.
 constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
 
-__global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const _Float16 *__restrict__ ns,
+// F32 (PDSC_PRECISION_F32): the Gram tiles on exact fp32 MFMA from the fp32
+// normed rows (`feats` = normed [B][N][128]); H3: `feats` = the split copy.
+template <bool F32>
+__global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict__ feats,
                                                        const float *__restrict__ src,
                                                        const float *__restrict__ tgt,
                                                        const int *__restrict__ knn, int N, int S, int k, int T,
@@ -486,21 +538,41 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const _Float16 *__rest
     // flight instead of both whole 32-row fragments): the wave fits in 128
     // VGPRs, 4 waves per SIMD to hide the row gathers.  Accumulation order per
     // tile is unchanged (k-steps ascending).
-    const _Float16 *F = ns + (size_t)b * N * 2 * CH;
     const int nt = (k + 31) / 32;
-    const _Float16 *r0 = F + (size_t)__shfl(idx, l32) * 2 * CH + 8 * h;
-    const _Float16 *r1 = F + (size_t)__shfl(idx, 32 + l32) * 2 * CH + 8 * h;
     f32x16 G00 = zero16(), G01 = zero16(), G11 = zero16();
+    if constexpr (F32) {
+        const float *F = static_cast<const float *>(feats) + (size_t)b * N * CH;
+        const float *r0 = F + (size_t)__shfl(idx, l32) * CH + 4 * h;
+        const float *r1 = F + (size_t)__shfl(idx, 32 + l32) * CH + 4 * h;
+#pragma unroll 4
+        for (int j = 0; j < CH / 8; ++j) {
+            const f32x4 av = *reinterpret_cast<const f32x4 *>(r0 + 8 * j);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const f16x8 ah = *reinterpret_cast<const f16x8 *>(r0 + 16 * j);
-        const f16x8 al = *reinterpret_cast<const f16x8 *>(r0 + CH + 16 * j);
-        G00 = mfma_h3(ah, al, ah, al, G00);
-        if (nt > 1) {
-            const f16x8 bh = *reinterpret_cast<const f16x8 *>(r1 + 16 * j);
-            const f16x8 bl = *reinterpret_cast<const f16x8 *>(r1 + CH + 16 * j);
-            G01 = mfma_h3(ah, al, bh, bl, G01);
-            G11 = mfma_h3(bh, bl, bh, bl, G11);
+            for (int e = 0; e < 4; ++e) G00 = mfma32(av[e], av[e], G00);
+            if (nt > 1) {
+                const f32x4 bv = *reinterpret_cast<const f32x4 *>(r1 + 8 * j);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    G01 = mfma32(av[e], bv[e], G01);
+                    G11 = mfma32(bv[e], bv[e], G11);
+                }
+            }
+        }
+    } else {
+        const _Float16 *F = static_cast<const _Float16 *>(feats) + (size_t)b * N * 2 * CH;
+        const _Float16 *r0 = F + (size_t)__shfl(idx, l32) * 2 * CH + 8 * h;
+        const _Float16 *r1 = F + (size_t)__shfl(idx, 32 + l32) * 2 * CH + 8 * h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const f16x8 ah = *reinterpret_cast<const f16x8 *>(r0 + 16 * j);
+            const f16x8 al = *reinterpret_cast<const f16x8 *>(r0 + CH + 16 * j);
+            G00 = mfma_h3(ah, al, ah, al, G00);
+            if (nt > 1) {
+                const f16x8 bh = *reinterpret_cast<const f16x8 *>(r1 + 16 * j);
+                const f16x8 bl = *reinterpret_cast<const f16x8 *>(r1 + CH + 16 * j);
+                G01 = mfma_h3(ah, al, bh, bl, G01);
+                G11 = mfma_h3(bh, bl, bh, bl, G11);
+            }
         }
     }
     __builtin_amdgcn_wave_barrier();  // P visible to the wave
@@ -548,14 +620,19 @@ size_t nsm_seed_lds_bytes(int k, int wpb) {
     return (size_t)wpb * (k * (k + 1) + KMAX * NSM_PSTR + KMAX) * sizeof(float);
 }
 
-hipError_t launch_nsm_seed(const _Float16 *ns, const float *src, const float *tgt, const int *knn, int B, int N,
-                           int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
+hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
+                           int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
                            unsigned *pair_mask, hipStream_t s) {
     if (k < 1 || k > KMAX) return hipErrorInvalidValue;
     const int wpb = seed_wpb(B, S);
-    hipLaunchKernelGGL(nsm_seed_kernel, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), nsm_seed_lds_bytes(k, wpb), s,
-                       ns, src, tgt, knn,
-                       N, S, k, T, sigma, sigma_d, hist, pair_mask);
+    const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
+    const size_t lds = nsm_seed_lds_bytes(k, wpb);
+    if (f32)
+        hipLaunchKernelGGL(nsm_seed_kernel<true>, grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma,
+                           sigma_d, hist, pair_mask);
+    else
+        hipLaunchKernelGGL(nsm_seed_kernel<false>, grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma,
+                           sigma_d, hist, pair_mask);
     return hipGetLastError();
 }
 

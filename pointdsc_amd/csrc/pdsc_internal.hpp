@@ -114,17 +114,20 @@ hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N
                                 float *Mp, hipStream_t s);
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
-                             const float *bn_rm, const float *bn_rv, int in, int out, float *dst_w,
+                             const float *bn_rm, const float *bn_rv, int in, int out, bool f32, float *dst_w,
                              float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s);
 hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 
 // Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
-int attention_nsplit(int B, int N);
-// q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element).
-// M: dense [B][N][N], or symmetric-packed [B][mpack_floats(N)] when m_packed.
-hipError_t launch_attention(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *M,
-                            bool m_packed, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+int attention_nsplit(int B, int N, bool f32);
+// q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
+// or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
+// M: dense [B][N][N], or symmetric-packed [B][mpack_floats(N)] when m_packed (H3 only).
+hipError_t launch_attention(const void *q, const void *k, const void *v, const float *M, bool m_packed,
+                            bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s);
+// fp32 rows [B][N][CH] -> [B][Npad][CH], padding rows zero.
+hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
 hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
                             _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s);
@@ -132,14 +135,13 @@ hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int 
 hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
                                int nsplit, float *msg, hipStream_t s);
 
-// Pointwise chains (one workgroup per PT points).
-hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, int B,
-                           int N, int Npad, float *feat, _Float16 *q, _Float16 *k, _Float16 *v,
-                           hipStream_t s);
-hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, _Float16 *q,
-                         _Float16 *k, _Float16 *v, hipStream_t s);
-hipError_t launch_pw_last(const float *packed, const PackLayout &lay, const float *opart,
+// Pointwise chains (one workgroup per PT points); q, k, v in launch_attention's layouts.
+hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
+                           int N, int Npad, float *feat, void *q, void *k, void *v, hipStream_t s);
+hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
+                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
+                         hipStream_t s);
+hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s);
 
@@ -152,10 +154,14 @@ hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, in
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s);
 hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s);
+// PDSC_PRECISION_F32 seed-row distances from the fp32 normed rows [B][N][128]
+hipError_t launch_knn_dist_f32(const float *normed, const int *seeds, int B, int N, int S, float *dist,
+                               hipStream_t s);
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s);
-// ns: the split normed copy [B][N][2][128] fp16 (as launch_knn_dist reads it)
-hipError_t launch_nsm_seed(const _Float16 *ns, const float *src, const float *tgt, const int *knn, int B, int N,
-                           int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
+// feats: the split normed copy [B][N][2][128] fp16 (as launch_knn_dist reads it),
+// or the fp32 normed rows [B][N][128] when f32
+hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
+                           int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
                            unsigned *pair_mask, hipStream_t s);
 hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B, int S, int k, int T,
                              float *weights, int *iters_used, hipStream_t s);

@@ -112,15 +112,18 @@ def encoder(cfg, packed, corr_pos, M, want_features=True):
     return feat, normed, conf
 
 
-def attention(q, k, v, M):
+def attention(q, k, v, M, precision="h3"):
     """softmax_j(M_ij q_i.k_j / sqrt(C)) v_j  (models/PointDSC.py:36-42); q,k,v [B,N,128]."""
     q, k, v, M = (_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (M, "M")))
     B, N, C = q.shape
+    if k.shape != q.shape or v.shape != q.shape or M.shape != (B, N, N):
+        raise ValueError(f"q {tuple(q.shape)} k {tuple(k.shape)} v {tuple(v.shape)} M {tuple(M.shape)}")
+    pc = _lib.precision_code(precision)
     L = _lib.load()
-    nb = L.pdsc_attention_workspace_bytes(B, N, C)
+    nb = L.pdsc_attention_workspace_bytes(B, N, C, pc)
     ws = _workspace(nb, q.device)
     msg = torch.empty_like(q)
-    check(L.pdsc_attention_f32(_p(q), _p(k), _p(v), _p(M), B, N, C, _p(msg), _p(ws), nb,
+    check(L.pdsc_attention_f32(_p(q), _p(k), _p(v), _p(M), B, N, C, pc, _p(msg), _p(ws), nb,
                                _stream(q.device)), "pdsc_attention_f32")
     return msg
 
@@ -138,7 +141,7 @@ def pick_seeds(src, conf, radius: float, max_num: int):
 
 
 # ---------------------------------------------------------------------- a6
-def seed_knn(normed, seeds, k: int):
+def seed_knn(normed, seeds, k: int, precision="h3"):
     """knn indices [B,S,k] int32 of the seed rows (models/common.py:48-69)."""
     normed, seeds = _dev(normed, "normed"), _dev(seeds, "seeds", torch.int32)
     B, N, C = normed.shape
@@ -147,13 +150,14 @@ def seed_knn(normed, seeds, k: int):
     nb = L.pdsc_seed_knn_workspace_bytes(B, N, S)
     ws = _workspace(nb, normed.device)
     out = torch.empty((B, S, k), dtype=torch.int32, device=normed.device)
-    check(L.pdsc_seed_knn(_p(normed), _p(seeds), B, N, C, S, int(k), _p(out), _p(ws), nb,
+    check(L.pdsc_seed_knn(_p(normed), _p(seeds), B, N, C, S, int(k), _lib.precision_code(precision), _p(out),
+                          _p(ws), nb,
                           _stream(normed.device)), "pdsc_seed_knn")
     return out
 
 
 # ------------------------------------------------------------------- a7-a8
-def nsm_weights(normed, src, tgt, knn, num_iterations, sigma, sigma_d):
+def nsm_weights(normed, src, tgt, knn, num_iterations, sigma, sigma_d, precision="h3"):
     """(weights [B,S,k], iterations used [B]) (models/PointDSC.py:257-282, :338-358)."""
     normed, src, tgt = _dev(normed, "normed"), _dev(src, "src"), _dev(tgt, "tgt")
     knn = _dev(knn, "knn", torch.int32)
@@ -166,7 +170,7 @@ def nsm_weights(normed, src, tgt, knn, num_iterations, sigma, sigma_d):
     w = torch.empty((B, S, k), dtype=torch.float32, device=normed.device)
     it = torch.empty((B,), dtype=torch.int32, device=normed.device)
     check(L.pdsc_nsm_weights(_p(normed), _p(src), _p(tgt), _p(knn), B, N, C, S, k, int(num_iterations),
-                             _p(sigma), _p(sigma_d), _p(w), _p(it), _p(ws), nb, _stream(normed.device)),
+                             _lib.precision_code(precision), _p(sigma), _p(sigma_d), _p(w), _p(it), _p(ws), nb, _stream(normed.device)),
           "pdsc_nsm_weights")
     return w, it
 
@@ -217,14 +221,20 @@ def post_refine(trans, src, tgt, thr: float):
 
 
 # ----------------------------------------------------------------- forward
+def _check_inputs(cfg, corr_pos, src, tgt):
+    """Shapes the forward kernels assume (the reference's Conv1d(in_dim) raises on a wrong width)."""
+    if src.dim() != 3 or src.shape[2] != 3 or tgt.shape != src.shape or corr_pos.dim() != 3 \
+            or corr_pos.shape[:2] != src.shape[:2] or corr_pos.shape[2] != cfg.in_dim:
+        raise ValueError(f"shape mismatch: corr_pos {tuple(corr_pos.shape)} (expected [B,N,{cfg.in_dim}]), "
+                         f"src {tuple(src.shape)}, tgt {tuple(tgt.shape)} (expected [B,N,3])")
+
+
 def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
     """Full testing forward for B pairs: (final_trans [B,4,4], final_labels [B,N])
     (+ (confidence [B,N], seeds [B,S]) when ``debug``)."""
     corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
     B, N, _ = src.shape
-    if corr_pos.shape[:2] != (B, N) or tgt.shape != src.shape:
-        raise ValueError(f"shape mismatch corr_pos {tuple(corr_pos.shape)} src {tuple(src.shape)} "
-                         f"tgt {tuple(tgt.shape)}")
+    _check_inputs(cfg, corr_pos, src, tgt)
     dev = src.device
     L = _lib.load()
     nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
@@ -264,6 +274,9 @@ class ForwardPlan:
         if getattr(self, "graph", None) is not None:
             self.graph.replay()
             return self.trans, self.labels
+        _check_inputs(self.cfg, corr_pos, src, tgt)
+        if tuple(src.shape[:2]) != (self.B, self.N):
+            raise ValueError(f"plan is for B={self.B} N={self.N}, got {tuple(src.shape[:2])}")
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else _stream(src.device)
         check(_lib.load().pdsc_forward_testing(
             ctypes.byref(self.cfg), _p(self.packed), _p(corr_pos), _p(src), _p(tgt), self.B, self.N,
