@@ -102,7 +102,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
 }
 
 struct EncBufs {
-    float *feat, *opart, *ml;
+    float *feat, *opart, *ml, *vexp;
     _Float16 *q, *k, *v;  // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
 };
 
@@ -115,21 +115,23 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
     e.v = c.take<_Float16>(2 * rows);
     e.opart = c.take<float>(rows * d.nsplit);
     e.ml = c.take<float>((size_t)d.B * d.Npad * d.nsplit * 2);
+    e.vexp = c.take<float>((size_t)d.B * (d.Npad / 32));
     return e;
 }
 
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
                 bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s) {
-    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, s));
+    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s));
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
-        HIPCHK(launch_attention(e.q, e.k, e.v, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
+                                s));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         if (l + 1 < lay.L)
             HIPCHK(launch_pw_mid(packed, lay, l, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
-                                 e.k, e.v, s));
+                                 e.k, e.v, e.vexp, s));
         else
             HIPCHK(launch_pw_last(packed, lay, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
                                   feat_out, normed, d.f32 ? nullptr : normed_s, conf, s));
@@ -357,6 +359,7 @@ size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C, int32_t p
     for (int i = 0; i < 3; ++i) c.take<_Float16>((size_t)2 * B * Npad * CH);
     c.take<float>((size_t)B * Npad * CH * ns);
     c.take<float>((size_t)B * Npad * ns * 2);
+    c.take<float>((size_t)B * (Npad / 32));
     return c.off;
 }
 
@@ -378,14 +381,15 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     _Float16 *vs = c.take<_Float16>((size_t)2 * B * Npad * CH);
     float *op = c.take<float>((size_t)B * Npad * CH * ns);
     float *ml = c.take<float>((size_t)B * Npad * ns * 2);
+    float *vexp = c.take<float>((size_t)B * (Npad / 32));
     if (f32) {  // the caller's rows, zero-padded to Npad rows (the same bytes as the split layouts)
         HIPCHK(launch_pad_rows(q, B, N, Npad, reinterpret_cast<float *>(qs), s));
         HIPCHK(launch_pad_rows(k, B, N, Npad, reinterpret_cast<float *>(ks), s));
         HIPCHK(launch_pad_rows(v, B, N, Npad, reinterpret_cast<float *>(vs), s));
     } else {  // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
-        HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, s));
+        HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, vexp, s));
     }
-    HIPCHK(launch_attention(qs, ks, vs, M, false, f32, B, N, Npad, ns, op, ml, s));
+    HIPCHK(launch_attention(qs, ks, vs, vexp, M, false, f32, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }

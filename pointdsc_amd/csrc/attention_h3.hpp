@@ -17,6 +17,12 @@
 // encoder are O(10)); a value outside turns the result into inf/NaN (loud,
 // never silently wrong).  Softmax weights are kept as p = 2^(x - m + PSHIFT)
 // <= 2^(DEFER + PSHIFT) = 2^15, so they too sit in fp16's normal range.
+// Small V: each 32-key tile of V is stored as V * 2^e (vexp[tile] = e in
+// [0, H3_VEXP_MAX], chosen by the producer from the tile's max |v|) so its lo
+// halves stay normal fp16; the tile's p are formed as 2^(x - m + PSHIFT - e)
+// (one add) and its sum re-scaled by 2^e (one ldexp): sum p v is unchanged.
+// Small Q or K only shrink the logits' absolute error, which is what the
+// softmax is sensitive to.
 //
 // HBM layouts (written by the pointwise kernels' epilogues, encoder.hip, or
 // by split_qkv_kernel for the standalone API), per pair, Npad rows:
@@ -50,6 +56,16 @@ constexpr int H3_KTB = H3_TILE * H3_ROWB;    // K tile bytes (16 KiB)
 constexpr int H3_VTB = 2 * CH * H3_TILE * 2; // V tile bytes (16 KiB)
 constexpr int H3_PSHIFT = 7;                 // p = 2^(x - m + PSHIFT)
 constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by > 2^8
+constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8 (p * 2^-e stays >= 2^-24 of the sum)
+
+// The V-tile exponent for a tile whose max |v| is vmax: the largest e <= 8 with
+// vmax 2^e < 2^14 (0 for vmax >= 2^13, vmax == 0 or non-finite vmax).
+PDSC_DEV int h3_vexp(float vmax) {
+    if (!(vmax > 0.0f) || !(vmax < 8192.0f)) return 0;
+    int ex;
+    frexpf(vmax, &ex);  // vmax < 2^ex
+    return max(0, min(H3_VEXP_MAX, 14 - ex));
+}
 
 // channel -> position in a Qs/Ks row: swap bits 2 and 3
 PDSC_DEV constexpr int qk_pos(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
@@ -85,6 +101,26 @@ PDSC_DEV f32x16 mfma_h3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x16 c) {
     return mfma_h(ah, bh, c);
 }
 
+// Products with a three-plane weight w = wh + wm + wl (every fp32 weight
+// exactly, encoder.hip: pack_dense_kernel) and a two-plane activation x = xh + xl:
+// x.w ~= xh.(wh + wm + wl) + xl.wh, small terms first.  The dropped xl.(wm + wl)
+// is 2^-22 relative and data-dependent; the weights themselves carry no
+// representation error (a 2-plane weight's 2^-23 error is the same perturbation
+// of the model for every point and measurably dominates the encoder's error).
+// mfma_xw3: A = activations (rows = points), B = weights; mfma_w3x: transposed.
+PDSC_DEV f32x16 mfma_xw3(f16x8 xh, f16x8 xl, f16x8 wh, f16x8 wm, f16x8 wl, f32x16 c) {
+    c = mfma_h(xh, wl, c);
+    c = mfma_h(xh, wm, c);
+    c = mfma_h(xl, wh, c);
+    return mfma_h(xh, wh, c);
+}
+PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x16 c) {
+    c = mfma_h(wl, xh, c);
+    c = mfma_h(wm, xh, c);
+    c = mfma_h(wh, xl, c);
+    return mfma_h(wh, xh, c);
+}
+
 template <int NW>
 constexpr size_t attention_h3_lds_bytes() { return (size_t)2 * (H3_KTB + H3_VTB); }
 
@@ -112,10 +148,12 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
 }
 
 // PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
+// vexp: [B][Npad/32] V-tile exponents (see above).
 template <int NW, bool XCD, bool PACKED>
 __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
-    const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart, float *__restrict__ ml) {
+    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
+    float *__restrict__ ml) {
     extern __shared__ __attribute__((aligned(16))) char h3smem[];
     // block -> (pair, query block, split), a pair's blocks kept on one XCD
     const int G = g.B * g.nqb * g.nsplit;
@@ -172,7 +210,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const float scale = 0.12751743082459868f;  // log2(e) / sqrt(128)
     const uint32_t Nb = (uint32_t)N * 4;
 
+    const float *vexp_b = vexp + (size_t)b * (Npad / H3_TILE);
     auto tile = [&](const char *Kl, const char *Vl, int key0) {
+        const float ev = vexp_b[key0 / H3_TILE];  // wave-uniform
         // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys, issued first
         float mv[16];
         if constexpr (PACKED) {
@@ -239,7 +279,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
                 for (int t = 0; t < 4; ++t) O[t][r] *= a;
             }
         }
-        const float mb = m_run - (float)H3_PSHIFT;
+        const float mb = m_run - (float)H3_PSHIFT + ev;
         float psum = 0.0f;
         f16x8 ph[2], pl[2];
 #pragma unroll
@@ -251,7 +291,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             ph[r >> 3][r & 7] = hi;
             pl[r >> 3][r & 7] = lo;
         }
-        l_run += psum;
+        l_run += ldexpf(psum, (int)ev);
         // O[query][4 l32 + t] += sum_key P[query][key] V[key][4 l32 + t]
         const int sw = (l32 >> 2) & 3;
 #pragma unroll
@@ -295,11 +335,29 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     }
 }
 
+// vexp of every 32-key tile of fp32 v [B][ld][CH] (rows >= N count as 0):
+// one workgroup per (tile, pair).
+static __global__ __launch_bounds__(256) void vexp_kernel(const float *__restrict__ v, int N, int ld, int Npad,
+                                                         float *__restrict__ vexp) {
+    __shared__ float part[4];
+    const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    float m = 0.0f;
+    for (int e = tid; e < H3_TILE * CH; e += 256) {
+        const int row = t * H3_TILE + e / CH;
+        if (row < N) m = fmaxf(m, fabsf(v[((size_t)b * ld + row) * CH + e % CH]));
+    }
+    m = wave_max(m);
+    if ((tid & 63) == 0) part[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) vexp[(size_t)b * (Npad / H3_TILE) + t] = (float)h3_vexp(fmaxf(fmaxf(part[0], part[1]), fmaxf(part[2], part[3])));
+}
+
 // fp32 q, k, v [B][ld][CH] (ld >= N rows per pair; rows >= N of the padded
-// layouts become zero) -> Qs, Ks, Vs.  One thread per (pair, row, channel).
+// layouts become zero) -> Qs, Ks, Vs (V scaled by its tile's 2^vexp).  One
+// thread per (pair, row, channel).
 static __global__ void split_qkv_kernel(const float *__restrict__ q, const float *__restrict__ k,
-                                 const float *__restrict__ v, int B, int N, int ld, int Npad,
-                                 _Float16 *__restrict__ Qs, _Float16 *__restrict__ Ks,
+                                 const float *__restrict__ v, const float *__restrict__ vexp, int B, int N,
+                                 int ld, int Npad, _Float16 *__restrict__ Qs, _Float16 *__restrict__ Ks,
                                  _Float16 *__restrict__ Vs) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)B * Npad * CH) return;
@@ -315,7 +373,8 @@ static __global__ void split_qkv_kernel(const float *__restrict__ q, const float
     split_h(in ? k[src] : 0.0f, hi, lo);
     Ks[pb + ks_off(row, 0, c)] = hi;
     Ks[pb + ks_off(row, 1, c)] = lo;
-    split_h(in ? v[src] : 0.0f, hi, lo);
+    const float ev = vexp[(size_t)b * (Npad / H3_TILE) + row / H3_TILE];
+    split_h(in ? ldexpf(v[src], (int)ev) : 0.0f, hi, lo);
     Vs[pb + vs_off(row, 0, c)] = hi;
     Vs[pb + vs_off(row, 1, c)] = lo;
 }

@@ -54,10 +54,14 @@ __global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w
     }
 }
 
-// W [out][in] (torch Conv1d weight) -> hi / lo fp16 planes of W * 2^s, same
-// [out][in] order: lane (h, n) of a 32x32x16 MFMA reads 8 consecutive inputs of
-// output n as one 16-B load (f32: W itself, fp32 [out][in]).  BN folded as
-// torch-CPU eval folds it.
+// W [out][in] (torch Conv1d weight) -> three fp16 planes hi, mid, lo of
+// W * 2^s = hi + mid + lo (33 significant bits: every fp32 weight exactly),
+// each [out][in] with the inputs of every 16-wide k-step in qk_pos order
+// (bits 2 and 3 of the index swapped): lane (h, n) of a 32x32x16 MFMA reads
+// positions 8h .. 8h+7 of output n as one 16-B load -- inputs {4h..4h+3,
+// 8+4h..8+4h+3} of the k-step, exactly the channels a transposed product's
+// accumulator half h holds (f32: W itself, fp32 [out][in], natural order).
+// BN folded as torch-CPU eval folds it.
 __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__restrict__ b,
                                   const float *__restrict__ bn_w, const float *__restrict__ bn_b,
                                   const float *__restrict__ bn_rm, const float *__restrict__ bn_rv,
@@ -69,11 +73,16 @@ __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__re
     if (i < total && f32) {
         dw[i] = w[i];
     } else if (i < total) {
-        _Float16 *wh = reinterpret_cast<_Float16 *>(dw), *wl = wh + total;
-        _Float16 hi, lo;
-        split_h(w[i] * sc[1], hi, lo);
-        wh[i] = hi;
-        wl[i] = lo;
+        _Float16 *wh = reinterpret_cast<_Float16 *>(dw), *wm = wh + total, *wl = wm + total;
+        const int o = i / in, c = i % in;
+        const int d = o * in + qk_pos(c);
+        const float x = w[i] * sc[1];  // exact (power of two)
+        const _Float16 hi = (_Float16)x;
+        const float r1 = x - (float)hi;  // exact
+        const _Float16 mid = (_Float16)r1;
+        wh[d] = hi;
+        wm[d] = mid;
+        wl[d] = (_Float16)(r1 - (float)mid);
     }
     if (i < out) {
         db[i] = b[i];
@@ -134,8 +143,8 @@ static AttnGrid f32_grid(int B, int N) { return attention_grid<ATT_NW, ATT_F32_K
 
 int attention_nsplit(int B, int N, bool f32) { return f32 ? f32_grid(B, N).nsplit : prod_grid(B, N).nsplit; }
 
-hipError_t launch_attention(const void *q, const void *k, const void *v, const float *M, bool m_packed,
-                            bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
+                            bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s) {
     if (f32) {  // fp32 [B][Npad][CH] rows, dense M
         const AttnGrid g = f32_grid(B, N);
@@ -153,10 +162,10 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     if (m_packed)
         hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), dim3(g.B * g.nqb * g.nsplit),
-                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, vexp, M, g, opart, ml);
     else
         hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), dim3(g.B * g.nqb * g.nsplit),
-                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, M, g, opart, ml);
+                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, vexp, M, g, opart, ml);
     return hipGetLastError();
 }
 
@@ -175,9 +184,10 @@ hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hip
 }
 
 hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
-                            _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s) {
+                            _Float16 *qs, _Float16 *ks, _Float16 *vs, float *vexp, hipStream_t s) {
     const size_t n = (size_t)B * Npad * CH;
-    hipLaunchKernelGGL(split_qkv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, k, v, B, N, ld,
+    hipLaunchKernelGGL(vexp_kernel, dim3(Npad / H3_TILE, B), dim3(256), 0, s, v, N, ld, Npad, vexp);
+    hipLaunchKernelGGL(split_qkv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, k, v, vexp, B, N, ld,
                        Npad, qs, ks, vs);
     return hipGetLastError();
 }
@@ -244,7 +254,7 @@ constexpr int IN_MAX = 16;  // layer0 input width held in registers
 // activations are read with the same map, so the products pair up).
 template <int IN, bool F32> struct WPanel;
 template <int IN> struct WPanel<IN, false> {
-    f16x8 h[IN / 16], l[IN / 16];
+    f16x8 h[IN / 16], m[IN / 16], l[IN / 16];
 };
 template <int IN> struct WPanel<IN, true> {
     f32x4 w[IN / 8];
@@ -259,19 +269,22 @@ PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int
         for (int j = 0; j < IN / 8; ++j) p.w[j] = *reinterpret_cast<const f32x4 *>(W + rowo + 8 * j);
     } else {
         const _Float16 *Wh = reinterpret_cast<const _Float16 *>(pk + off.w);
-        const _Float16 *Wl = Wh + (size_t)OUT * IN;
+        const _Float16 *Wm = Wh + (size_t)OUT * IN, *Wl = Wm + (size_t)OUT * IN;
         const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 8 * (lane >> 5);
 #pragma unroll
         for (int ks = 0; ks < IN / 16; ++ks) {
             p.h[ks] = *reinterpret_cast<const f16x8 *>(Wh + rowo + 16 * ks);
+            p.m[ks] = *reinterpret_cast<const f16x8 *>(Wm + rowo + 16 * ks);
             p.l[ks] = *reinterpret_cast<const f16x8 *>(Wl + rowo + 16 * ks);
         }
     }
 }
 
-// 8 consecutive fp32 activations (LDS, 16-B aligned) -> hi / lo fp16 fragments
-PDSC_DEV void split8(const float *x, f16x8 &hi, f16x8 &lo) {
-    const f32x4 a = *reinterpret_cast<const f32x4 *>(x), b = *reinterpret_cast<const f32x4 *>(x + 4);
+// The 8 fp32 activations at positions 8h .. 8h+7 of the k-step starting at x
+// (qk_pos order: channels 4h..4h+3 and 8+4h..8+4h+3; LDS, 16-B aligned) ->
+// hi / lo fp16 fragments.
+PDSC_DEV void split8(const float *x, int h, f16x8 &hi, f16x8 &lo) {
+    const f32x4 a = *reinterpret_cast<const f32x4 *>(x + 4 * h), b = *reinterpret_cast<const f32x4 *>(x + 8 + 4 * h);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         _Float16 p, q;
@@ -309,14 +322,14 @@ PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, 
             }
         }
     } else {
-        const float *xp = X + (rt0 * 32 + l32) * xstr + 8 * h;
+        const float *xp = X + (rt0 * 32 + l32) * xstr;
 #pragma unroll
         for (int ks = 0; ks < IN / 16; ++ks) {
 #pragma unroll
             for (int i = 0; i < NRT; ++i) {
                 f16x8 xh, xl;
-                split8(xp + i * 32 * xstr + 16 * ks, xh, xl);
-                acc[i] = mfma_h3(xh, xl, wp.h[ks], wp.l[ks], acc[i]);
+                split8(xp + i * 32 * xstr + 16 * ks, h, xh, xl);
+                acc[i] = mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[ks], acc[i]);
             }
         }
     }
@@ -369,18 +382,22 @@ PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
     const int r = tid / TPR;
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
-        const int c = (tid % TPR) * CPT + q;
+        const int c = (tid % TPR) * CPT + q;  // chunk c = positions 8c .. 8c+7 (qk_pos order)
         f16x8 hi, lo;
-        split8(X + r * xstr + 8 * c, hi, lo);
+        split8(X + r * xstr + 16 * (c >> 1), c & 1, hi, lo);
         const int o = r * XS_ROWB + 16 * (c ^ (r & 15));
         *reinterpret_cast<f16x8 *>(Xs + o) = hi;
         *reinterpret_cast<f16x8 *>(Xs + o + CH * 2) = lo;
     }
 }
 
+// SPLIT_V also sets the tile exponents vexp[p0/32 + i] (attention_h3.hpp) from
+// the max |v| over the 4 waves' channel tiles, exchanged through `red` (LDS,
+// 4 * NRT floats no other wave reads at this point; one barrier).
 template <int MODE, int NRT>
 PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const float *__restrict__ pk,
-                          const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane) {
+                          const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane,
+                          float *red = nullptr, float *__restrict__ vexp = nullptr) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
 #pragma unroll
@@ -393,14 +410,32 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
             const char *xr = Xs + r * XS_ROWB + 16 * ((2 * ks + h) ^ (r & 15));
             const f16x8 xh = *reinterpret_cast<const f16x8 *>(xr);
             const f16x8 xl = *reinterpret_cast<const f16x8 *>(xr + CH * 2);
-            acc[i] = MODE == SPLIT_V ? mfma_h3(xh, xl, wp.h[ks], wp.l[ks], acc[i])
-                                     : mfma_h3(wp.h[ks], wp.l[ks], xh, xl, acc[i]);
+            acc[i] = MODE == SPLIT_V ? mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[ks], acc[i])
+                                     : mfma_w3x(wp.h[ks], wp.m[ks], wp.l[ks], xh, xl, acc[i]);
         }
     }
     const float inv = pk[off.scale];
     if constexpr (MODE == SPLIT_V) {
         const int c = ct * 32 + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
         const float bias = pk[off.bias + c];
+        int ev[NRT];
+#pragma unroll
+        for (int i = 0; i < NRT; ++i) {
+            float m = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[i][r] = acc[i][r] * inv + bias;
+                m = fmaxf(m, fabsf(acc[i][r]));
+            }
+            m = wave_max(m);
+            if (lane == 0) red[4 * i + ct] = m;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NRT; ++i) {
+            ev[i] = h3_vexp(fmaxf(fmaxf(red[4 * i], red[4 * i + 1]), fmaxf(red[4 * i + 2], red[4 * i + 3])));
+            if (ct == 0 && lane == 0) vexp[(p0 >> 5) + i] = (float)ev[i];
+        }
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
             _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * (2 * CH * H3_TILE) + rho * H3_TILE;
@@ -410,7 +445,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     _Float16 a, b;
-                    split_h(acc[i][8 * s + e] * inv + bias, a, b);
+                    split_h(ldexpf(acc[i][8 * s + e], ev[i]), a, b);
                     hi[e] = a;
                     lo[e] = b;
                 }
@@ -491,7 +526,7 @@ template <int PTT> constexpr size_t pw_lds() { return (size_t)(2 * PTT * S132) *
 template <int PTT, bool F32>
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                      _Float16 *__restrict__ V, int p0, int tid, int wave, int lane) {
+                      _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane) {
     // four 128 -> 128 products with the same wave -> output-tile map (ct = wave):
     // each one's weight panel is fetched while the previous one computes
     WPanel<CH, F32> pa, pb;
@@ -522,7 +557,7 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
         load_wpanel<CH, CH, F32>(pk, d.v, wave, lane, pb);
         asm volatile("" ::: "memory");
         dense_split<SPLIT_K, PTT / 32>(Xs, pa, pk, d.k, wave, K, p0, lane);
-        dense_split<SPLIT_V, PTT / 32>(Xs, pb, pk, d.v, wave, V, p0, lane);
+        dense_split<SPLIT_V, PTT / 32>(Xs, pb, pk, d.v, wave, V, p0, lane, Xout, vexp);  // Xout is dead
     }
 }
 
@@ -533,7 +568,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
                                                        const float *__restrict__ corr, int in_dim,
                                                        int N, int Npad, float *__restrict__ feat,
                                                        _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                                                       _Float16 *__restrict__ V) {
+                                                       _Float16 *__restrict__ V, float *__restrict__ vexp) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PTT * S132, *cp = XB;  // cp: [PTT][in_dim], consumed before XB is written
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
@@ -558,7 +593,8 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
         XA[p * S132 + j] = s + bj;
     }
     __syncthreads();
-    pcn_qkv<PTT, F32>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    pcn_qkv<PTT, F32>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
@@ -598,7 +634,7 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
                                                      const float *__restrict__ ml, int nsplit, int N,
                                                      int Npad, float *__restrict__ feat,
                                                      _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                                                     _Float16 *__restrict__ V) {
+                                                     _Float16 *__restrict__ V, float *__restrict__ vexp) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PTT * S132, *XC = XB;
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
@@ -607,7 +643,8 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
-    pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff, p0, tid, wave, lane);
+    pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
 }
 
 template <int PTT, bool F32>
@@ -708,20 +745,20 @@ static bool small_tiles(int B, int Npad) {
     } while (0)
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
-                           int N, int Npad, float *feat, void *q, void *k, void *v, hipStream_t s) {
+                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     PW_LAUNCH(pw_first_kernel, Npad, packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad,
-              feat, Q, K, V);
+              feat, Q, K, V, vexp);
     return hipGetLastError();
 }
 
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
-                         hipStream_t s) {
+                         float *vexp, hipStream_t s) {
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,
-              N, Npad, feat, Q, K, V);
+              N, Npad, feat, Q, K, V, vexp);
     return hipGetLastError();
 }
 

@@ -34,13 +34,14 @@ inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 //   W  : OUT*IN floats in MFMA fragment order:
 //        Wpk[((jt*(IN/8) + g)*64 + lane)*4 + e] = W[jt*32 + (lane&31)][(lane>>5)*(IN/2) + 4g + e]
 //   bias[OUT], alpha[OUT], beta[OUT]   (alpha=1, beta=0 when no BN)
-// A dense layer in the packed blob: W as two fp16 planes [out][in] (hi, lo:
-// W * 2^s = hi + lo, s chosen per layer so max|W| 2^s <= 2^14) occupying the
-// out*in floats at w, then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
+// A dense layer in the packed blob: W as three fp16 planes [out][in] (hi, mid,
+// lo: W * 2^s = hi + mid + lo, s chosen per layer so max|W| 2^s <= 2^14, inputs
+// of each 16-wide k-step in qk_pos order) occupying 1.5*out*in floats at w --
+// or, for PDSC_PRECISION_F32, W itself fp32 [out][in] in the first out*in of
+// them -- then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
 struct DenseOff {
     size_t w, bias, alpha, beta, scale;
 };
-inline size_t dense_floats(int in, int out) { return (size_t)out * in + 3 * (size_t)out + 4; }
 
 struct LayerOff {
     DenseOff pcn, fc0, fc3, fc6, q, k, v;
@@ -60,7 +61,7 @@ struct PackLayout {
 inline DenseOff dense_at(size_t &o, int in, int out) {
     DenseOff d;
     d.w = o;
-    o += (size_t)out * in;
+    o += (size_t)out * in * 3 / 2;
     d.bias = o;
     o += out;
     d.alpha = o;
@@ -123,24 +124,25 @@ int attention_nsplit(int B, int N, bool f32);
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
 // or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
 // M: dense [B][N][N], or symmetric-packed [B][mpack_floats(N)] when m_packed (H3 only).
-hipError_t launch_attention(const void *q, const void *k, const void *v, const float *M, bool m_packed,
-                            bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+// vexp: [B][Npad/32] V-tile exponents of the H3 layout (attention_h3.hpp); unused for f32.
+hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
+                            bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s);
 // fp32 rows [B][N][CH] -> [B][Npad][CH], padding rows zero.
 hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
 hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
-                            _Float16 *qs, _Float16 *ks, _Float16 *vs, hipStream_t s);
+                            _Float16 *qs, _Float16 *ks, _Float16 *vs, float *vexp, hipStream_t s);
 // Combine partials -> msg [B][Npad][CH] (used by the standalone attention API).
 hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
                                int nsplit, float *msg, hipStream_t s);
 
 // Pointwise chains (one workgroup per PT points); q, k, v in launch_attention's layouts.
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
-                           int N, int Npad, float *feat, void *q, void *k, void *v, hipStream_t s);
+                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s);
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
-                         hipStream_t s);
+                         float *vexp, hipStream_t s);
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s);
