@@ -714,6 +714,548 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     }
 }
 
+// ============================================== pw2: register-chained pointwise chain
+// The large-launch form of pw_first / pw_mid / pw_last (H3 precision).  A
+// workgroup is PW2_W waves; wave w owns the 32 consecutive points p0 + 32 w ..
+// +31 (lane l32 <-> point: one MFMA tile) and carries their whole per-point
+// chain in registers.  Dense layers run transposed, Y^T = W X^T (A = weights,
+// B = activations): accumulator register r of lane (h, l32) of output tile t is
+// channel 32 t + acc_row(r, h) of point l32, and registers 8u .. 8u+7 of tile t
+// are exactly the fragment of k-step 2t + u that the next layer's B operand
+// takes (inputs in qk_pos order -- the packed weights' order), so layers chain
+// with no data movement between lanes.  V runs untransposed (A = activations,
+// B = weights) to come out in the attention's V-tile layout.
+//
+// Weights: blocks (one 32-output tile x one 16-input k-step: hi, mid, lo
+// planes, 1 KiB each) copied into LDS by LDS-DMA, PW2_CB blocks per chunk,
+// double-buffered and shared by the workgroup's waves; the chunk after the one
+// being multiplied is in flight meanwhile.  Per-channel epilogue coefficients
+// (bias, BN alpha / beta) of every layer of the kernel sit in LDS for the
+// whole launch.  Two workgroups per CU (~53 KiB of LDS and <= 256 VGPRs each)
+// overlap one's HBM phases with the other's MFMAs.
+//
+// Barriers: each chunk ends with "s_waitcnt vmcnt(n); s_barrier" where n
+// counts only the global stores issued after that chunk's DMA -- a layer's
+// output stores are issued by the NEXT layer right after it has queued its
+// first DMA (the `pre` hook), so no barrier waits on a store.
+constexpr int PW2_W = 4;                              // waves per workgroup: 128 points
+constexpr int PW2_CB = 8;                             // blocks per chunk (24 KiB)
+constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 planes)
+constexpr int PW2_PTS = PW2_W * 32;
+constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
+constexpr size_t PW2_LDS = 2 * PW2_CB * PW2_BLKB + PW2_COEF * sizeof(float);
+
+struct W2Chunk {  // blocks (t, ks), t in [t0, t0 + nt), ks in [0, in / 16), of one packed layer
+    const _Float16 *w;
+    int in, out, t0, nt;
+};
+
+PDSC_DEV W2Chunk w2_chunk(const float *pk, const DenseOff &o, int in, int out, int t0, int nt) {
+    return W2Chunk{reinterpret_cast<const _Float16 *>(pk + o.w), in, out, t0, nt};
+}
+// output tiles per chunk of an IN -> OUT layer
+constexpr int w2_nt(int in, int out) {
+    return PW2_CB / (in / 16) < 1 ? 1 : (PW2_CB / (in / 16) < out / 32 ? PW2_CB / (in / 16) : out / 32);
+}
+
+// LDS-DMA of one chunk: piece (blk, plane) = 1 KiB = one wave instruction, lane
+// (h, n) fetching inputs 8h .. 8h+7 of output 32 t + n -- the reader's lane
+// reads the same 16 B back at 16 * lane (lane-linear, conflict-free).
+PDSC_DEV void w2_stage(const W2Chunk &c, char *slot, int wave, int lane) {
+    const int nks = c.in / 16, npieces = c.nt * nks * 3;
+    const size_t plane_sz = (size_t)c.out * c.in;
+    const _Float16 *base = c.w + (size_t)(32 * c.t0 + (lane & 31)) * c.in + 8 * (lane >> 5);
+    for (int i = wave; i < npieces; i += PW2_W) {
+        const int blk = i / 3, plane = i - 3 * blk;
+        const int t = blk / nks, ks = blk - t * nks;
+        __builtin_amdgcn_global_load_lds(base + plane * plane_sz + (size_t)(32 * t) * c.in + 16 * ks,
+                                         slot + (blk * 3 + plane) * 1024, 16, 0, 0);
+    }
+}
+
+// acc[t0 + t] += W_t X for the chunk's NT tiles x NKS k-steps (TRANS: A = W, B =
+// X); the fragments of block j + 1 are read while block j's MFMAs run, and the
+// empty asm keeps the compiler from hoisting further reads (registers).
+template <int NKS, int NT, bool TRANS, int NACC>
+PDSC_DEV void w2_mma(const char *slot, const f16x8 *xh, const f16x8 *xl, f32x16 (&acc)[NACC], int t0, int lane) {
+    const char *bp = slot + 16 * lane;
+    f16x8 w0 = *reinterpret_cast<const f16x8 *>(bp), w1 = *reinterpret_cast<const f16x8 *>(bp + 1024),
+          w2 = *reinterpret_cast<const f16x8 *>(bp + 2048);
+#pragma unroll
+    for (int j = 0; j < NT * NKS; ++j) {
+        const int t = j / NKS, ks = j % NKS;
+        f16x8 n0 = w0, n1 = w1, n2 = w2;
+        if (j + 1 < NT * NKS) {
+            const char *np = bp + (j + 1) * PW2_BLKB;
+            n0 = *reinterpret_cast<const f16x8 *>(np);
+            n1 = *reinterpret_cast<const f16x8 *>(np + 1024);
+            n2 = *reinterpret_cast<const f16x8 *>(np + 2048);
+        }
+        acc[t0 + t] = TRANS ? mfma_w3x(w0, w1, w2, xh[ks], xl[ks], acc[t0 + t])
+                            : mfma_xw3(xh[ks], xl[ks], w0, w1, w2, acc[t0 + t]);
+        asm volatile("" ::: "memory");
+        w0 = n0;
+        w1 = n1;
+        w2 = n2;
+    }
+}
+
+struct W2Pipe {  // the two LDS slots; chunk c is multiplied from `cur` while c + 1 lands in `nxt`
+    char *cur, *nxt;
+    PDSC_DEV void swap() {
+        char *t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+};
+
+// End of a chunk: this wave's DMA pieces have landed (all but its `nst` youngest
+// vector-memory ops, the stores issued after them, are done) and its LDS reads
+// of the chunk have returned, then the barrier.
+template <int NST>
+PDSC_DEV void w2_sync(bool active) {
+    if (NST > 0 && active)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+struct W2NoPre {
+    PDSC_DEV void operator()() const {}
+};
+
+// One dense layer IN -> OUT: per chunk, queue the next chunk (or `after`, the
+// next layer's first), run `pre` once (the previous layer's NST stores), multiply,
+// sync.  P.cur must hold this layer's first chunk.
+template <int IN, int OUT, bool TRANS, int NST = 0, typename PRE = W2NoPre>
+PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const DenseOff &o, const W2Chunk *after, const f16x8 *xh,
+                       const f16x8 *xl, f32x16 (&acc)[OUT / 32], bool active, int wave, int lane,
+                       const PRE &pre = PRE()) {
+    constexpr int NKS = IN / 16, NT = w2_nt(IN, OUT), NCH = OUT / 32 / NT;
+    static_assert(NCH * NT == OUT / 32, "chunk tiling");
+#pragma unroll
+    for (int t = 0; t < OUT / 32; ++t) acc[t] = zero16();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        if (c + 1 < NCH)
+            w2_stage(w2_chunk(pk, o, IN, OUT, (c + 1) * NT, NT), P.nxt, wave, lane);
+        else if (after)
+            w2_stage(*after, P.nxt, wave, lane);
+        asm volatile("" ::: "memory");
+        if (c == 0) {
+            pre();
+            if (active) w2_mma<NKS, NT, TRANS>(P.cur, xh, xl, acc, 0, lane);
+            w2_sync<NST>(active);
+        } else {
+            if (active) w2_mma<NKS, NT, TRANS>(P.cur, xh, xl, acc, c * NT, lane);
+            w2_sync<0>(active);
+        }
+        P.swap();
+    }
+}
+
+// The epilogue coefficients (bias, alpha, beta: 3 * out contiguous floats from
+// DenseOff::bias) of one layer into LDS at `dst`.
+PDSC_DEV void w2_coef(float *dst, const float *__restrict__ pk, const DenseOff &o, int out, int tid) {
+    for (int i = tid; i < 3 * out; i += PW2_W * 64) dst[i] = pk[o.bias + i];
+}
+
+// fp32 -> fp16 hi / lo of 8 values
+PDSC_DEV void split8v(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        _Float16 a, b;
+        split_h(v[e], a, b);
+        hi[e] = a;
+        lo[e] = b;
+    }
+}
+
+// Channel of register 8u + e of output tile t for lane half h (transposed layout).
+PDSC_DEV int w2_chan(int t, int u, int e, int h) { return 32 * t + 16 * u + 8 * (e >> 2) + 4 * h + (e & 3); }
+
+// Epilogue of a transposed layer: y = epi(acc 2^-s + b) (EPI_BIAS / RELU /
+// BN_RELU, as dense_tile_w; EPI_RESID adds resid[t][r]) back into acc, and
+// (SPLIT) the hi / lo split of every k-step fragment into xh / xl.  cf = the
+// layer's LDS coefficients (bias[out], alpha[out], beta[out]).  SPLIT is a
+// compile-time flag: a run-time null test of xh would keep the caller's arrays
+// out of registers.
+template <int OUT, int EPI, bool SPLIT = true>
+PDSC_DEV void w2_epilogue(f32x16 (&acc)[OUT / 32], float inv, const float *cf, const f32x16 *resid, f16x8 *xh,
+                          f16x8 *xl, int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < OUT / 32; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c0 = 32 * t + 16 * u + 4 * h;
+            const f32x4 b0 = *reinterpret_cast<const f32x4 *>(cf + c0), b1 = *reinterpret_cast<const f32x4 *>(cf + c0 + 8);
+            f32x4 a0, a1, e0, e1;
+            if (EPI == EPI_BN_RELU) {
+                a0 = *reinterpret_cast<const f32x4 *>(cf + OUT + c0);
+                a1 = *reinterpret_cast<const f32x4 *>(cf + OUT + c0 + 8);
+                e0 = *reinterpret_cast<const f32x4 *>(cf + 2 * OUT + c0);
+                e1 = *reinterpret_cast<const f32x4 *>(cf + 2 * OUT + c0 + 8);
+            }
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int r = 8 * u + e;
+                float y = __builtin_fmaf(acc[t][r], inv, e < 4 ? b0[e] : b1[e - 4]);  // exact acc 2^-s, one rounding
+                if (EPI == EPI_BN_RELU) y = fmaxf(y * (e < 4 ? a0[e] : a1[e - 4]) + (e < 4 ? e0[e] : e1[e - 4]), 0.0f);
+                if (EPI == EPI_RELU) y = fmaxf(y, 0.0f);
+                if (EPI == EPI_RESID) y = resid[t][r] + y;  // res = feat + message (:44)
+                acc[t][r] = y;
+                v[e] = y;
+            }
+            if constexpr (SPLIT) split8v(v, xh[2 * t + u], xl[2 * t + u]);
+        }
+}
+
+// Combine the split partials of this lane's point into the k-step fragments of
+// the 128 message channels (as combine16: sum_s w_s O_s / sum_s w_s l_s).
+PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restrict__ ml, int b, int nsplit, int Npad,
+                         int row, f16x8 *xh, f16x8 *xl, int h) {
+    float mstar = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[((size_t)(b * nsplit + s) * Npad + row) * 2]);
+    float L = 0.0f;
+    f32x4 acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s = 0; s < nsplit; ++s) {
+        const size_t base = (size_t)(b * nsplit + s) * Npad + row;
+        const float w = expf(ml[base * 2] - mstar);
+        L += w * ml[base * 2 + 1];
+        const float *src = opart + base * CH + 4 * h;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            acc[2 * ks] += w * *reinterpret_cast<const f32x4 *>(src + 16 * ks);
+            acc[2 * ks + 1] += w * *reinterpret_cast<const f32x4 *>(src + 16 * ks + 8);
+        }
+    }
+    const float rl = 1.0f / L;  // the softmax denominator once (the reference divides e by its sum first)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[e] = acc[2 * ks][e] * rl;
+            v[4 + e] = acc[2 * ks + 1][e] * rl;
+        }
+        split8v(v, xh[ks], xl[ks]);
+    }
+}
+
+// This lane's 64 fp32 values of a 128-channel row (featL: [Npad][2][64], the
+// lane-register order of a transposed 128-output layer): 16 x 16 B each way.
+PDSC_DEV void w2_load_row(const float *__restrict__ featL, int row, int h, f32x16 (&y)[4]) {
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(featL + ((size_t)row * 2 + h) * 64);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 v = src[4 * t + q];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[t][4 * q + e] = v[e];
+        }
+}
+PDSC_DEV void w2_store_row(float *__restrict__ featL, int row, int h, const f32x16 (&y)[4]) {
+    f32x4 *dst = reinterpret_cast<f32x4 *>(featL + ((size_t)row * 2 + h) * 64);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[4 * t + q] = f32x4{y[t][4 * q], y[t][4 * q + 1], y[t][4 * q + 2], y[t][4 * q + 3]};
+}
+
+// Q / K outputs (transposed, bias only; 16 stores) in the attention_h3 row
+// layouts: registers 8u .. 8u+7 of tile t = qk_pos positions 32t + 16u + 8h .. +7.
+template <bool SWZ>
+PDSC_DEV void w2_store_qk(const f32x16 (&acc)[4], float inv, const float *bias, _Float16 *__restrict__ dst, int row,
+                          int lane) {
+    const int h = lane >> 5;
+    _Float16 *drow = dst + (size_t)row * 2 * CH;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c0 = 32 * t + 16 * u + 4 * h;
+            const f32x4 b0 = *reinterpret_cast<const f32x4 *>(bias + c0), b1 = *reinterpret_cast<const f32x4 *>(bias + c0 + 8);
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(acc[t][8 * u + e], inv, e < 4 ? b0[e] : b1[e - 4]);
+            f16x8 hi, lo;
+            split8v(v, hi, lo);
+            int chk = 4 * t + 2 * u + h;
+            if (SWZ) chk ^= row & 15;
+            *reinterpret_cast<f16x8 *>(drow + 8 * chk) = hi;
+            *reinterpret_cast<f16x8 *>(drow + CH + 8 * chk) = lo;
+        }
+}
+
+// V output (untransposed: lane l32 <-> channel 32t + l32, register r <-> point
+// acc_row(r, h) of the wave's key tile) into the tile's V planes, scaled by the
+// tile's 2^vexp (the tile's max |v| is wave-local here).
+PDSC_DEV void w2_store_v(f32x16 (&acc)[4], float inv, const float *bias, _Float16 *__restrict__ Vt,
+                         float *__restrict__ vexp_t, int lane) {
+    const int h = lane >> 5, l32 = lane & 31;
+    float m = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float bs = bias[32 * t + l32];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            acc[t][r] = __builtin_fmaf(acc[t][r], inv, bs);
+            m = fmaxf(m, fabsf(acc[t][r]));
+        }
+    }
+    const int ev = h3_vexp(wave_max(m));
+    if (lane == 0) *vexp_t = (float)ev;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int c = 32 * t + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
+        _Float16 *prow = Vt + rho * H3_TILE;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ldexpf(acc[t][8 * s + e], ev);
+            f16x8 hi, lo;
+            split8v(v, hi, lo);
+            const int chk = (2 * s + h) ^ sw;
+            *reinterpret_cast<f16x8 *>(prow + 8 * chk) = hi;
+            *reinterpret_cast<f16x8 *>(prow + CH * H3_TILE + 8 * chk) = lo;
+        }
+    }
+}
+
+// LDS coefficient table of a PointCN + QKV stage (PW2_COEF floats available).
+struct W2CoefQKV {
+    static constexpr int pcn = 0, q = 3 * CH, k = 4 * CH, v = 5 * CH, end = 6 * CH;
+};
+PDSC_DEV void w2_coef_qkv(float *cf, const float *pk, const PwDense4 &d, int tid) {
+    w2_coef(cf + W2CoefQKV::pcn, pk, d.pcn, CH, tid);
+    for (int i = tid; i < CH; i += PW2_W * 64) {  // Q / K / V: bias only
+        cf[W2CoefQKV::q + i] = pk[d.q.bias + i];
+        cf[W2CoefQKV::k + i] = pk[d.k.bias + i];
+        cf[W2CoefQKV::v + i] = pk[d.v.bias + i];
+    }
+}
+
+// PointCN (BN, ReLU) of the fragments x, then the Q/K/V projections; the
+// PointCN rows go to featL.  Expects P.cur = the PCN layer's first chunk;
+// `pre` = the caller's pending stores (NST of them), issued in the PCN layer.
+template <int NST, typename PRE>
+PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const float *cf, const PwDense4 &d, const f16x8 *xh,
+                         const f16x8 *xl, float *__restrict__ featL, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                         _Float16 *__restrict__ V, float *__restrict__ vexp, int row, bool active, int wave, int lane,
+                         const PRE &pre) {
+    const int h = lane >> 5;
+    f32x16 ap[4], aq[4];
+    f16x8 yh[8], yl[8];
+    const W2Chunk q0 = w2_chunk(pk, d.q, CH, CH, 0, w2_nt(CH, CH)), k0 = w2_chunk(pk, d.k, CH, CH, 0, w2_nt(CH, CH)),
+                  v0 = w2_chunk(pk, d.v, CH, CH, 0, w2_nt(CH, CH));
+    const float sp = pk[d.pcn.scale], sq = pk[d.q.scale], sk = pk[d.k.scale], sv = pk[d.v.scale];
+    w2_layer<CH, CH, true, NST>(P, pk, d.pcn, &q0, xh, xl, ap, active, wave, lane, pre);
+    if (active) w2_epilogue<CH, EPI_BN_RELU>(ap, sp, cf + W2CoefQKV::pcn, nullptr, yh, yl, lane);
+    w2_layer<CH, CH, true, 16>(P, pk, d.q, &k0, yh, yl, aq, active, wave, lane, [&] {
+        if (active) w2_store_row(featL, row, h, ap);
+    });
+    w2_layer<CH, CH, true, 16>(P, pk, d.k, &v0, yh, yl, ap, active, wave, lane, [&] {
+        if (active) w2_store_qk<false>(aq, sq, cf + W2CoefQKV::q, Q, row, lane);
+    });
+    w2_layer<CH, CH, false, 16>(P, pk, d.v, nullptr, yh, yl, aq, active, wave, lane, [&] {
+        if (active) w2_store_qk<true>(ap, sk, cf + W2CoefQKV::k, K, row, lane);
+    });
+    if (active) w2_store_v(aq, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * (2 * CH * H3_TILE), vexp + (row >> 5), lane);
+}
+
+#define PW2_PROLOGUE                                                                              \
+    extern __shared__ __attribute__((aligned(16))) char w2smem[];                                 \
+    const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5; \
+    const int row = blockIdx.x * PW2_PTS + wave * 32 + (lane & 31);                               \
+    const bool active = blockIdx.x * PW2_PTS + wave * 32 < Npad; /* wave-uniform */               \
+    const size_t boff = (size_t)b * Npad * CH;                                                    \
+    W2Pipe P{w2smem, w2smem + PW2_CB * PW2_BLKB};                                                 \
+    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_CB * PW2_BLKB);
+
+// layer0 (Conv1d in_dim -> 128 on exact fp32 MFMA 32x32x2, k-step j: inputs 2j + h)
+// + PointCN_0 + QKV_0.
+__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *__restrict__ pk, size_t l0w, size_t l0b,
+                                                                 PwDense4 d, const float *__restrict__ corr, int in_dim,
+                                                                 int N, int Npad, float *__restrict__ featL,
+                                                                 _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                                                                 _Float16 *__restrict__ V, float *__restrict__ vexp) {
+    PW2_PROLOGUE
+    const int l32 = lane & 31;
+    w2_stage(w2_chunk(pk, d.pcn, CH, CH, 0, w2_nt(CH, CH)), P.cur, wave, lane);
+    w2_coef_qkv(cf, pk, d, tid);
+    f16x8 xh[8], xl[8];
+    if (active) {
+        const float *cp = corr + ((size_t)b * N + min(row, N - 1)) * in_dim;
+        const bool in = row < N;
+        f32x16 acc[4] = {zero16(), zero16(), zero16(), zero16()};
+        for (int j = 0; j < (in_dim + 1) / 2; ++j) {
+            const int i = 2 * j + h;
+            const float x = (in && i < in_dim) ? cp[i] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float w = i < in_dim ? pk[l0w + (32 * t + l32) * in_dim + i] : 0.0f;
+                acc[t] = mfma32(w, x, acc[t]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = acc[t][8 * u + e] + pk[l0b + w2_chan(t, u, e, h)];
+                split8v(v, xh[2 * t + u], xl[2 * t + u]);
+            }
+    }
+    __syncthreads();
+    w2_pcn_qkv<0>(P, pk, cf, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane, W2NoPre());
+}
+
+// combine_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1}.
+__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
+                                                               const float *__restrict__ opart,
+                                                               const float *__restrict__ ml, int nsplit, int N,
+                                                               int Npad, float *__restrict__ featL,
+                                                               _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                                                               _Float16 *__restrict__ V, float *__restrict__ vexp) {
+    PW2_PROLOGUE
+    constexpr int CF0 = W2CoefQKV::end, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2;
+    static_assert(CF6 + 3 * CH <= PW2_COEF, "coefficient table");
+    w2_stage(w2_chunk(pk, m.fc0, CH, CH2, 0, w2_nt(CH, CH2)), P.cur, wave, lane);
+    w2_coef_qkv(cf, pk, d, tid);
+    w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
+    w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
+    w2_coef(cf + CF6, pk, m.fc6, CH, tid);
+    f16x8 xh[8], xl[8];
+    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
+    __syncthreads();
+    const W2Chunk fc3 = w2_chunk(pk, m.fc3, CH2, CH2, 0, w2_nt(CH2, CH2)), fc6 = w2_chunk(pk, m.fc6, CH2, CH, 0, w2_nt(CH2, CH)),
+                  pcn = w2_chunk(pk, d.pcn, CH, CH, 0, w2_nt(CH, CH));
+    f32x16 a2[2], a4[4], res[4];
+    f16x8 yh[8], yl[8];
+    w2_layer<CH, CH2, true>(P, pk, m.fc0, &fc3, xh, xl, a2, active, wave, lane);
+    if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + CF0, nullptr, yh, yl, lane);
+    w2_layer<CH2, CH2, true>(P, pk, m.fc3, &fc6, yh, yl, a2, active, wave, lane);
+    if (active) {
+        w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
+        w2_load_row(featL + boff, row, h, res);  // the residual: lands during fc6's MFMAs
+    }
+    w2_layer<CH2, CH, true>(P, pk, m.fc6, &pcn, xh, xl, a4, active, wave, lane);
+    if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);
+    w2_pcn_qkv<0>(P, pk, cf, d, yh, yl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane, W2NoPre());
+}
+
+// combine + fc_message + residual, then F.normalize (:156) and the classifier (:171).
+__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
+    const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
+    const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
+    const float *__restrict__ featL, float *__restrict__ feat_out, float *__restrict__ normed,
+    _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
+    PW2_PROLOGUE
+    constexpr int CF0 = 0, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2, CC0 = CF6 + 3 * CH, CC2 = CC0 + 3 * CLS,
+                  CC4 = CC2 + 3 * CLS;
+    static_assert(CC4 + CLS <= PW2_COEF, "coefficient table");
+    w2_stage(w2_chunk(pk, m.fc0, CH, CH2, 0, w2_nt(CH, CH2)), P.cur, wave, lane);
+    w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
+    w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
+    w2_coef(cf + CF6, pk, m.fc6, CH, tid);
+    w2_coef(cf + CC0, pk, c0, CLS, tid);
+    w2_coef(cf + CC2, pk, c2, CLS, tid);
+    for (int i = tid; i < CLS; i += PW2_W * 64) cf[CC4 + i] = pk[c4w + i];
+    f16x8 xh[8], xl[8];
+    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
+    __syncthreads();
+    const W2Chunk fc3 = w2_chunk(pk, m.fc3, CH2, CH2, 0, w2_nt(CH2, CH2)), fc6 = w2_chunk(pk, m.fc6, CH2, CH, 0, w2_nt(CH2, CH)),
+                  cc0 = w2_chunk(pk, c0, CH, CLS, 0, w2_nt(CH, CLS)), cc2 = w2_chunk(pk, c2, CLS, CLS, 0, w2_nt(CLS, CLS));
+    f32x16 a1[1], a2[2], a4[4], res[4];
+    f16x8 yh[8], yl[8];
+    w2_layer<CH, CH2, true>(P, pk, m.fc0, &fc3, xh, xl, a2, active, wave, lane);
+    if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + CF0, nullptr, yh, yl, lane);
+    w2_layer<CH2, CH2, true>(P, pk, m.fc3, &fc6, yh, yl, a2, active, wave, lane);
+    if (active) {
+        w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
+        w2_load_row(featL + boff, row, h, res);
+    }
+    w2_layer<CH2, CH, true>(P, pk, m.fc6, &cc0, xh, xl, a4, active, wave, lane);
+    const bool in = row < N;
+    float den = 1.0f;
+    if (active) {
+        w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);  // a4 = corr_features (:155)
+        float ss = 0.0f;  // F.normalize(p=2, dim=-1, eps=1e-12) (:156)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ss = __builtin_fmaf(a4[t][r], a4[t][r], ss);
+        ss += __shfl_xor(ss, 32);
+        den = fmaxf(sqrtf(ss), 1e-12f);
+    }
+    // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171);
+    // the feature / normed stores are issued inside the first classifier layer
+    w2_layer<CH, CLS, true, 32>(P, pk, c0, &cc2, yh, yl, a1, active, wave, lane, [&] {
+        if (!active || !in) return;
+        float *dst = normed + ((size_t)b * N + row) * CH;
+        _Float16 *ds = normed_s ? normed_s + ((size_t)b * N + row) * 2 * CH : nullptr;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = a4[t][8 * u + e] / den;
+                *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 4 * h) = f32x4{v[0], v[1], v[2], v[3]};
+                *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 8 + 4 * h) = f32x4{v[4], v[5], v[6], v[7]};
+                if (ds) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
+                    f16x8 hi, lo;
+                    split8v(v, hi, lo);
+                    const int chk = 4 * t + 2 * u + h;
+                    *reinterpret_cast<f16x8 *>(ds + 8 * chk) = hi;
+                    *reinterpret_cast<f16x8 *>(ds + CH + 8 * chk) = lo;
+                }
+            }
+        if (feat_out) {  // natural channel order (the standalone encoder API only)
+            float *fo = feat_out + ((size_t)b * N + row) * CH;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *reinterpret_cast<f32x4 *>(fo + 32 * t + 8 * g + 4 * h) =
+                        f32x4{a4[t][4 * g], a4[t][4 * g + 1], a4[t][4 * g + 2], a4[t][4 * g + 3]};
+        }
+    });
+    if (active) w2_epilogue<CLS, EPI_RELU>(a1, pk[c0.scale], cf + CC0, nullptr, xh, xl, lane);
+    w2_layer<CLS, CLS, true>(P, pk, c2, nullptr, xh, xl, a1, active, wave, lane);
+    if (active) {
+        w2_epilogue<CLS, EPI_RELU, false>(a1, pk[c2.scale], cf + CC2, nullptr, nullptr, nullptr, lane);
+        float s = 0.0f;  // this half's 16 channels, then the other half's
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s = __builtin_fmaf(cf[CC4 + w2_chan(0, u, e, h)], a1[0][8 * u + e], s);
+        s += __shfl_xor(s, 32);
+        if (in && h == 0) conf[(size_t)b * N + row] = s + pk[c4b];
+    }
+}
+#undef PW2_PROLOGUE
+
+// pw2 for launches of at least two 128-point workgroups per CU (knob PDSC_PW2:
+// 0 never, 2 always, else this rule; measurement only).
+static bool use_pw2(int B, int Npad, bool f32) {
+    static const int mode = [] {
+        const char *e = getenv("PDSC_PW2");
+        return e ? atoi(e) : 1;
+    }();
+    if (f32 || mode == 0) return false;
+    return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) >= 512;
+}
+
 static PwDense4 dense4(const LayerOff &l) { return PwDense4{l.pcn, l.q, l.k, l.v}; }
 static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
@@ -748,6 +1290,12 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
                            int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
+    if (use_pw2(B, Npad, f32)) {
+        hipLaunchKernelGGL(pw2_first_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
+                           packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K,
+                           V, vexp);
+        return hipGetLastError();
+    }
     PW_LAUNCH(pw_first_kernel, Npad, packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad,
               feat, Q, K, V, vexp);
     return hipGetLastError();
@@ -757,6 +1305,12 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
                          float *vexp, hipStream_t s) {
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
+    if (use_pw2(B, Npad, f32)) {
+        hipLaunchKernelGGL(pw2_mid_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
+                           packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad,
+                           feat, Q, K, V, vexp);
+        return hipGetLastError();
+    }
     PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,
               N, Npad, feat, Q, K, V, vexp);
     return hipGetLastError();
@@ -765,6 +1319,12 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s) {
+    if (use_pw2(B, Npad, f32)) {
+        hipLaunchKernelGGL(pw2_last_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
+                           packed, msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N,
+                           Npad, feat, feat_out, normed, normed_s, conf);
+        return hipGetLastError();
+    }
     PW_LAUNCH(pw_last_kernel, N, packed, msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml,
               nsplit, N, Npad, feat, feat_out, normed, normed_s, conf);
     return hipGetLastError();

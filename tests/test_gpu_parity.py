@@ -1,31 +1,43 @@
-"""HIP path vs the reference's golden vectors and the CPU oracle (run with -m gpu).
+"""HIP path vs the reference's golden vectors, an exact-arithmetic (fp64) yardstick
+and the CPU oracle (run with -m gpu).
 
-Tolerances (north_star): inlier masks / seeds / kNN / fitness bit-exact;
-confidences and poses within 1e-4 (fp32).  Every call goes through the C ABI
-(libpdsc.so) via pointdsc_amd.kernels."""
+Bars (north_star):
+  * index / mask work bit-exact: M, is_local_max, NMS, kNN selection, fitness,
+    final_labels -- up to the near-ties fp32 re-ordering is free to decide
+    either way, which every such check names explicitly;
+  * poses within 1e-4;
+  * encoder features / confidences: within ENVELOPE x the reference's OWN
+    distance from exact arithmetic (conftest.py): the reference itself sits up to
+    4e-4 (logits) from exact math on these goldens, so a literal 1e-4 against it
+    is below fp32's resolution for this network.
+Both precision modes are held to the same bars.  Every call goes through the C
+ABI (libpdsc.so) via pointdsc_amd.kernels."""
 import numpy as np
 import pytest
 import torch
 
-from conftest import (assert_close_scaled, assert_knn_equivalent, assert_seeds_equivalent, golden_hparams, golden_names,
-                      golden_state_dict, load_golden)
+from conftest import (ENVELOPE, FEAT_FLOOR, LOGIT_FLOOR, assert_knn_equivalent, assert_rigid, assert_seeds_equivalent,
+                      assert_seeds_near_ties, encoder_fp64, golden_hparams, golden_names, golden_state_dict,
+                      load_golden, seed_H_rank)
 
 pytestmark = pytest.mark.gpu
 
 NAMES = golden_names()
+PRECISIONS = ["h3", "f32"]
 POSE_ATOL = 1e-4
+_FP64 = {}
 
 
 def _t(x, dev, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(x)).to(dev, dtype)
 
 
-def _model(g, dev):
+def _model(g, dev, precision="h3"):
     from pointdsc_amd.PointDSC import PointDSC
     hp = golden_hparams(g)
     m = PointDSC(in_dim=6, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
                  inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
-                 nms_radius=hp["nms_radius"])
+                 nms_radius=hp["nms_radius"], precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state_dict(g).items()})
     return m.to(dev).eval()
 
@@ -34,32 +46,86 @@ def _inputs(g, dev):
     return (_t(g["corr_pos"][None], dev), _t(g["src_keypts"][None], dev), _t(g["tgt_keypts"][None], dev))
 
 
+def _fp64(name, g, dev):
+    if name not in _FP64:
+        _FP64[name] = encoder_fp64(g, golden_state_dict(g), dev)
+    return _FP64[name]
+
+
+def _envelope(name, g, dev):
+    """(feature error bound x max|f|, logit error bound) vs exact arithmetic, and the yardstick."""
+    f64, c64 = _fp64(name, g, dev)
+    mx = np.abs(f64).max()
+    e_c = np.abs(g["confidence"] - c64).max()
+    if len(g["corr_features"]):
+        e_f = np.abs(g["corr_features"] - f64).max() / mx
+    else:  # N > 5000 goldens keep the logits only
+        e_f = None
+    return e_f, e_c, f64, c64, mx
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_compat(name, gpu_device):
     from pointdsc_amd import kernels
     g = load_golden(name)
     _, src, tgt = _inputs(g, gpu_device)
     sd = torch.tensor([float(g["sigma_d"])], dtype=torch.float32, device=gpu_device)
-    M = kernels.compat(src, tgt, sd)[0].cpu().numpy()
+    M = kernels.compat(src, tgt, sd)[0]
     if "M" in g:
-        assert np.array_equal(M, g["M"])  # bit-exact
-    assert np.array_equal(np.diagonal(M), g["M_diag"])
-    assert np.array_equal(M, M.T)
-    np.testing.assert_allclose(M.astype(np.float64).sum(-1), g["M_row_sums"], rtol=1e-12, atol=1e-9)
+        assert np.array_equal(M.cpu().numpy(), g["M"])  # bit-exact
+    assert np.array_equal(torch.diagonal(M).cpu().numpy(), g["M_diag"])
+    assert torch.equal(M, M.T)
+    np.testing.assert_allclose(M.double().sum(-1).cpu().numpy(), g["M_row_sums"], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", NAMES)
-def test_encoder_and_classifier(name, gpu_device):
+def test_encoder_and_classifier(name, precision, gpu_device):
+    """a2-a4: features, normed features and logits within ENVELOPE x the reference's
+    own distance from exact arithmetic (plus an fp32-resolution floor)."""
     from pointdsc_amd import kernels
     g = load_golden(name)
-    m = _model(g, gpu_device)
+    m = _model(g, gpu_device, precision)
     corr, src, tgt = _inputs(g, gpu_device)
     M = kernels.compat(src, tgt, m.sigma_spat)
     feat, normed, conf = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, M)
-    assert_close_scaled(feat[0].cpu().numpy(), g["corr_features"])
-    np.testing.assert_allclose(conf[0].cpu().numpy(), g["confidence"], rtol=1e-5, atol=1e-3)
-    ref_n = g["corr_features"] / np.maximum(np.linalg.norm(g["corr_features"], axis=1, keepdims=True), 1e-12)
-    np.testing.assert_allclose(normed[0].cpu().numpy(), ref_n, atol=1e-4)  # unit vectors
+    e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
+    ours_c = np.abs(conf[0].double().cpu().numpy() - c64).max()
+    assert ours_c <= ENVELOPE * e_c + LOGIT_FLOOR, (ours_c, e_c)
+    f = feat[0].double().cpu().numpy()
+    ours_f = np.abs(f - f64).max() / mx
+    if e_f is not None:
+        assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (ours_f, e_f)
+    else:
+        assert ours_f <= 5e-5, ours_f  # no reference features stored (N > 5000): absolute fp32-level bound
+    n64 = f64 / np.maximum(np.linalg.norm(f64, axis=1, keepdims=True), 1e-12)
+    e_n = (np.abs(g["corr_features"] / np.maximum(np.linalg.norm(g["corr_features"], axis=1, keepdims=True), 1e-12)
+                  - n64).max() if e_f is not None else 5e-5)
+    assert np.abs(normed[0].double().cpu().numpy() - n64).max() <= ENVELOPE * e_n + FEAT_FLOOR
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_h3_matches_exact_fp32(name, gpu_device):
+    """The 3xfp16 contractions against the exact-fp32 MFMA mode on the same inputs:
+    features and logits within the same envelope, identical labels, poses 1e-4."""
+    from pointdsc_amd import kernels
+    g = load_golden(name)
+    corr, src, tgt = _inputs(g, gpu_device)
+    out = {}
+    for p in PRECISIONS:
+        m = _model(g, gpu_device, p)
+        M = kernels.compat(src, tgt, m.sigma_spat)
+        feat, _, conf = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, M)
+        T, L = kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr, src, tgt)
+        out[p] = (feat[0].double().cpu().numpy(), conf[0].double().cpu().numpy(), T[0].cpu().numpy(),
+                  L[0].cpu().numpy())
+    e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
+    (fh, ch, Th, Lh), (ff, cf, Tf, Lf) = out["h3"], out["f32"]
+    ef = e_f if e_f is not None else 2e-5
+    assert np.abs(fh - ff).max() / mx <= ENVELOPE * ef + FEAT_FLOOR
+    assert np.abs(ch - cf).max() <= ENVELOPE * e_c + LOGIT_FLOOR
+    assert np.array_equal(Lh, Lf)
+    np.testing.assert_allclose(Th, Tf, atol=POSE_ATOL)
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -74,31 +140,41 @@ def test_pick_seeds_exact(name, gpu_device):
     assert_seeds_equivalent(seeds[0].cpu().numpy(), g["seeds"], g["confidence"] * g["is_local_max"])
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", NAMES)
-def test_nsm_chain(name, gpu_device):
-    """a6-a11, each stage fed with the reference's inputs for that stage."""
+def test_nsm_chain(name, precision, gpu_device):
+    """a6-a11, each stage fed with the reference's inputs for that stage.  Seeds
+    whose covariance H has rank < 2 (collinear / duplicated neighbourhoods: the
+    rotation is LAPACK's arbitrary choice in a one-parameter family) are held to
+    the rigid-transform properties instead of the reference's pose."""
     from pointdsc_amd import kernels
     g = load_golden(name)
     sd = golden_state_dict(g)
     _, src, tgt = _inputs(g, gpu_device)
-    f = g["corr_features"]
-    nrm = f / np.maximum(np.linalg.norm(f, axis=1, keepdims=True), 1e-12)
-    normed = _t(nrm, gpu_device)[None]
-    seeds = _t(g["seeds"][None], gpu_device, torch.int32)
-    k = g["knn_idx"].shape[1]
-    knn = kernels.seed_knn(normed, seeds, k)
-    assert_knn_equivalent(knn[0].cpu().numpy(), g["knn_idx"], nrm, g["seeds"])
-    ref_knn = _t(g["knn_idx"][None], gpu_device, torch.int32)
-    sigma = _t(sd["sigma"], gpu_device)
-    sigma_d = _t(sd["sigma_spat"], gpu_device)
-    w, iters = kernels.nsm_weights(normed, src, tgt, ref_knn, 10, sigma, sigma_d)
+    if len(g["corr_features"]):
+        f = g["corr_features"]
+        nrm = f / np.maximum(np.linalg.norm(f, axis=1, keepdims=True), 1e-12)
+        normed = _t(nrm, gpu_device)[None]
+        seeds = _t(g["seeds"][None], gpu_device, torch.int32)
+        k = g["knn_idx"].shape[1]
+        knn = kernels.seed_knn(normed, seeds, k, precision=precision)
+        assert_knn_equivalent(knn[0].cpu().numpy(), g["knn_idx"], nrm, g["seeds"])
+        ref_knn = _t(g["knn_idx"][None], gpu_device, torch.int32)
+        w, iters = kernels.nsm_weights(normed, src, tgt, ref_knn, 10, _t(sd["sigma"], gpu_device),
+                                       _t(sd["sigma_spat"], gpu_device), precision=precision)
+        v = g["leading_eig"]
+        np.testing.assert_allclose(w[0].cpu().numpy(), v / (v.sum(-1, keepdims=True) + 1e-6), atol=2e-5)
     v = g["leading_eig"]
-    np.testing.assert_allclose(w[0].cpu().numpy(), v / (v.sum(-1, keepdims=True) + 1e-6), atol=2e-5)
-    w_ref = _t((v / (v.sum(-1, keepdims=True) + np.float32(1e-6)))[None], gpu_device)
-    seed_trans, fit, best, trans, labels = kernels.seed_hypotheses(src, tgt, ref_knn, w_ref,
+    w_ref = (v / (v.sum(-1, keepdims=True) + np.float32(1e-6))).astype(np.float32)
+    ref_knn = _t(g["knn_idx"][None], gpu_device, torch.int32)
+    seed_trans, fit, best, trans, labels = kernels.seed_hypotheses(src, tgt, ref_knn, _t(w_ref[None], gpu_device),
                                                                    float(g["inlier_threshold"]))
-    np.testing.assert_allclose(seed_trans[0].cpu().numpy(), g["seed_trans"], atol=POSE_ATOL)
-    assert np.array_equal(fit[0].cpu().numpy(), g["seed_fitness"])
+    st = seed_trans[0].cpu().numpy()
+    ok = seed_H_rank(g) > 1e-5
+    np.testing.assert_allclose(st[ok], g["seed_trans"][ok], atol=POSE_ATOL)
+    for s in np.nonzero(~ok)[0]:
+        assert_rigid(st[s], g["src_keypts"][g["knn_idx"][s]], g["tgt_keypts"][g["knn_idx"][s]], w_ref[s])
+    assert np.array_equal(fit[0].cpu().numpy()[ok], g["seed_fitness"][ok])
     np.testing.assert_allclose(trans[0].cpu().numpy(), g["trans_pre_refine"], atol=POSE_ATOL)
     assert np.array_equal(labels[0].cpu().numpy(), g["final_labels"])
     thr = 0.10 if float(g["inlier_threshold"]) == 0.10 else 1.2
@@ -106,11 +182,13 @@ def test_nsm_chain(name, gpu_device):
     np.testing.assert_allclose(ref[0].cpu().numpy(), g["final_trans"], atol=POSE_ATOL)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("name", NAMES)
-def test_module_forward_end_to_end(name, gpu_device):
-    """PointDSC.forward(data) with 'testing' -- the drop-in contract."""
+def test_module_forward_end_to_end(name, precision, gpu_device):
+    """PointDSC.forward(data) with 'testing' -- the drop-in contract: labels
+    bit-exact, pose within 1e-4."""
     g = load_golden(name)
-    m = _model(g, gpu_device)
+    m = _model(g, gpu_device, precision)
     corr, src, tgt = _inputs(g, gpu_device)
     with torch.no_grad():
         res = m({"corr_pos": corr, "src_keypts": src, "tgt_keypts": tgt, "testing": True})
@@ -120,35 +198,62 @@ def test_module_forward_end_to_end(name, gpu_device):
     np.testing.assert_allclose(res["final_trans"][0].cpu().numpy(), g["final_trans"], atol=POSE_ATOL)
 
 
-@pytest.mark.parametrize("name", ["rel_1k", "rel_1k_kitti"])
-def test_debug_outputs_match_reference(name, gpu_device):
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("name", NAMES)
+def test_forward_seeds_near_ties(name, precision, gpu_device):
+    """The seeds the full forward picks (a5 on our own confidences) equal the
+    reference's except where a local-max decision or a ranking swap involves two
+    reference confidences closer than twice our measured logit error."""
     from pointdsc_amd import kernels
     g = load_golden(name)
-    m = _model(g, gpu_device)
+    m = _model(g, gpu_device, precision)
     corr, src, tgt = _inputs(g, gpu_device)
     trans, labels, conf, seeds = kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr, src, tgt,
                                                          debug=True)
-    np.testing.assert_allclose(conf[0].cpu().numpy(), g["confidence"], rtol=1e-5, atol=1e-3)
-    ours = set(seeds[0].cpu().numpy().tolist())
-    assert len(ours & set(g["seeds"].tolist())) >= 0.98 * len(g["seeds"])
+    conf = conf[0].cpu().numpy()
+    tol = float(np.abs(conf - g["confidence"]).max())
+    _, e_c, _, _, _ = _envelope(name, g, gpu_device)
+    assert tol <= (ENVELOPE + 1) * e_c + LOGIT_FLOOR  # |ours - ref| <= |ours - exact| + |ref - exact|
+    flips, moved = assert_seeds_near_ties(seeds[0].cpu().numpy(), conf, g, tol)
+    assert moved <= 4 * flips + 0.1 * len(g["seeds"])
 
 
-def test_batched_equals_single(gpu_device):
-    """B pairs in one call == B single-pair calls (labels bitwise; poses within
-    the north-star pose tolerance: the attention's split-K over keys depends on
-    B, so the softmax partials combine in a different fp32 order)."""
+def test_kabsch_degenerate_goldens(gpu_device):
+    """rigid_transform_3d on the reference's own degenerate cases
+    (tests/golden/kabsch_degenerate.npz): zero / negative weights (H = 0 -> the
+    reference's R = I), three points and coplanar points (rank-2 H: unique R) are
+    pinned at 1e-4; rank-1 H (collinear, duplicated points) by the properties."""
+    from pointdsc_amd import kernels
+    from conftest import GOLDEN
+    import os
+    z = np.load(os.path.join(GOLDEN, "kabsch_degenerate.npz"))
+    names = sorted({k.split("__")[0] for k in z.files})
+    for n in names:
+        A, B, w, T = z[n + "__A"], z[n + "__B"], z[n + "__w"], z[n + "__T"]
+        ours = kernels.rigid_transform_3d(_t(A[None], gpu_device), _t(B[None], gpu_device),
+                                          _t(w[None], gpu_device))[0].cpu().numpy()
+        if bool(z[n + "__pinned"]):
+            np.testing.assert_allclose(ours, T, atol=POSE_ATOL, err_msg=n)
+        else:
+            assert_rigid(ours, A.astype(np.float64), B.astype(np.float64), w)
+
+
+@pytest.mark.parametrize("B", [6, 24, 64])
+def test_batched_equals_single(B, gpu_device):
+    """B pairs in one call == B single-pair calls: labels bitwise, poses within
+    twice the north-star tolerance (the batched launches take other kernel
+    variants: B = 24 the 4-wave seed kernels (B*ceil(S/4) >= 512), B = 64 also
+    the register-chained pointwise kernels; fp32 sums in another order)."""
     from pointdsc_amd.synthetic import synthetic_batch
     g = load_golden("rel_1k")
     m = _model(g, gpu_device)
-    b = synthetic_batch(6, 1000, seed=5)
+    b = synthetic_batch(B, 1000, seed=5)
     corr, src, tgt = (_t(b[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
     T, Lb = m.forward_batched(corr, src, tgt)
-    for i in range(6):
+    for i in range(B):
         r = m({"corr_pos": corr[i:i + 1], "src_keypts": src[i:i + 1], "tgt_keypts": tgt[i:i + 1],
                "testing": True})
-        assert torch.equal(r["final_labels"][0], Lb[i])
-        # two fp32 evaluation orders of the same pair (split-K differs with B), each
-        # within POSE_ATOL of the reference on the goldens: allow twice that between them
+        assert torch.equal(r["final_labels"][0], Lb[i]), i
         np.testing.assert_allclose(r["final_trans"][0].cpu().numpy(), T[i].cpu().numpy(), atol=2 * POSE_ATOL)
 
 
@@ -197,8 +302,13 @@ def test_graph_replay_equals_eager(gpu_device):
         hip.hipEventDestroy(ctypes.c_void_p(ev[i]))
 
 
-def test_attention_vs_torch_fp32(gpu_device):
-    """The attention kernel against a plain PyTorch fp32 reference of :36-42."""
+def _attention_fp64(q, k, v, M):
+    return torch.softmax(M.double() * (q.double() @ k.double().transpose(1, 2)) / 128 ** 0.5, -1) @ v.double()
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_attention_vs_torch_fp64(precision, gpu_device):
+    """The attention core (:36-42) against a plain PyTorch fp64 evaluation."""
     from pointdsc_amd import kernels
     torch.manual_seed(0)
     for B, N in [(1, 1000), (2, 333), (1, 4096)]:
@@ -206,9 +316,40 @@ def test_attention_vs_torch_fp32(gpu_device):
         src = torch.rand(B, N, 3, device=gpu_device) * 3
         tgt = src + 0.05 * torch.randn(B, N, 3, device=gpu_device)
         M = kernels.compat(src, tgt, torch.tensor([0.1], device=gpu_device))
-        out = kernels.attention(q, k, v, M)
-        ref = torch.softmax(M.double() * (q.double() @ k.double().transpose(1, 2)) / 128 ** 0.5, -1) @ v.double()
-        np.testing.assert_allclose(out.cpu().numpy(), ref.float().cpu().numpy(), rtol=1e-4, atol=2e-5)
+        out = kernels.attention(q, k, v, M, precision=precision).double()
+        ref = _attention_fp64(q, k, v, M)
+        assert (out - ref).abs().max().item() <= 1e-6 * v.abs().max().item()
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("sv", [1e-3, 1.0, 1e2])
+@pytest.mark.parametrize("sqk", [(1e-3, 1e-3), (7.0, 1.0), (1e2, 1e-1)])
+def test_attention_adversarial_magnitudes(sqk, sv, precision, gpu_device):
+    """Operand magnitudes far from the encoder's O(1): Q, K scaled so the logits are
+    ~1e-6 or spread over ~+-20 (softmax weights over > 2^50, i.e. > 30 log2
+    units), V scaled by 1e-3 .. 1e2.  Error bound relative to max|V| (the output's
+    scale); the 3xfp16 path keeps small V exact through its per-tile exponent."""
+    from pointdsc_amd import kernels
+    torch.manual_seed(1)
+    B, N = 2, 700
+    sq, sk = sqk
+    q = torch.randn(B, N, 128, device=gpu_device) * sq
+    k = torch.randn(B, N, 128, device=gpu_device) * sk
+    v = torch.randn(B, N, 128, device=gpu_device) * sv
+    v[:, ::7] *= 1e-3  # rows of very different magnitude inside one 32-key tile
+    src = torch.rand(B, N, 3, device=gpu_device) * 3
+    tgt = src + 0.02 * torch.randn(B, N, 3, device=gpu_device)
+    M = kernels.compat(src, tgt, torch.tensor([0.1], device=gpu_device))
+    lg = M.double() * (q.double() @ k.double().transpose(1, 2)) / 128 ** 0.5
+    spread = (lg.max(-1).values - lg.min(-1).values).max().item()
+    if sq * sk > 1:
+        assert spread > 30 * np.log(2)
+    out = kernels.attention(q, k, v, M, precision=precision).double()
+    ref = _attention_fp64(q, k, v, M)
+    # logits of magnitude L carry fp32 rounding ~2^-24 L in both the reference and here,
+    # and the softmax turns an absolute logit error into that relative weight error
+    tol = 2e-6 + 4 * 2.0 ** -24 * max(1.0, lg.abs().max().item())
+    assert (out - ref).abs().max().item() <= tol * v.abs().max().item()
 
 
 def test_rigid_transform_vs_oracle(gpu_device):
@@ -225,10 +366,11 @@ def test_rigid_transform_vs_oracle(gpu_device):
         np.testing.assert_allclose(T, O.rigid_transform_3d(A, Bp, w), atol=2e-5)
 
 
-@pytest.mark.parametrize("preset", ["3dmatch", "kitti"])
-def test_full_size_registration_properties(preset, gpu_device):
-    """N=5000, B=4 (BASELINE sizes): the recovered pose matches ground truth and
-    every label set is the inlier set of the returned pre-refinement pose."""
+@pytest.mark.parametrize("preset,N,B", [("3dmatch", 5000, 4), ("kitti", 5000, 4), ("kitti", 12000, 1)])
+def test_full_size_registration_properties(preset, N, B, gpu_device):
+    """BASELINE sizes and the KITTI driver's largest (num_node=12000,
+    evaluation/test_KITTI.py:151): the recovered pose matches ground truth and
+    every label is 0/1 with most inliers found."""
     from pointdsc_amd.synthetic import PRESETS, synthetic_batch, trained_state_dict
     from pointdsc_amd.PointDSC import PointDSC
     p = PRESETS[preset]
@@ -236,11 +378,11 @@ def test_full_size_registration_properties(preset, gpu_device):
                  nms_radius=p["nms_radius"])
     m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict(preset).items()})
     m = m.to(gpu_device).eval()
-    b = synthetic_batch(4, 5000, seed=77, preset=preset)
+    b = synthetic_batch(B, N, seed=77, preset=preset)
     corr, src, tgt = (_t(b[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
     T, labels = m.forward_batched(corr, src, tgt)
     T, labels = T.cpu().numpy(), labels.cpu().numpy()
-    for i in range(4):
+    for i in range(B):
         gt = b["gt_trans"][i]
         cosang = (np.trace(T[i, :3, :3].T @ gt[:3, :3]) - 1) / 2
         re = np.degrees(np.arccos(np.clip(cosang, -1, 1)))
@@ -248,6 +390,34 @@ def test_full_size_registration_properties(preset, gpu_device):
         assert re < 1.0 and te < 0.2 * p["inlier_threshold"] * 10, (re, te)
         assert labels[i].sum() >= 0.9 * b["gt_labels"][i].sum()
         assert set(np.unique(labels[i])) <= {0.0, 1.0}
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_recall_parity_synthetic(precision, gpu_device):
+    """Registration-recall parity proxy (the 3DMatch recall claim needs data and
+    weights absent here): on 64 FPFH-like pairs (6 % inliers, N = 1000) the HIP
+    path and the CPU oracle succeed (RE < 15 deg, TE < 30 cm, libs/loss.py:44-51)
+    on exactly the same pairs."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd.evaluate import pair_stats
+    from pointdsc_amd.synthetic import synthetic_batch, trained_state_dict
+    g = load_golden("rel_1k")
+    m = _model(g, gpu_device, precision)
+    b = synthetic_batch(64, 1000, seed=606, inlier_ratio=0.06)
+    corr, src, tgt = (_t(b[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    T, L = m.forward_batched(corr, src, tgt)
+    ours = pair_stats(T.cpu(), torch.from_numpy(b["gt_trans"]), L.cpu(), torch.from_numpy(b["gt_labels"]))
+    sd = golden_state_dict(g)
+    hp = golden_hparams(g)
+    ref_T, ref_L = [], []
+    for i in range(64):
+        o = O.forward_testing(b["corr_pos"][i], b["src_keypts"][i], b["tgt_keypts"][i], sd, **hp)
+        ref_T.append(o["final_trans"])
+        ref_L.append(o["final_labels"])
+    ref = pair_stats(torch.from_numpy(np.stack(ref_T)), torch.from_numpy(b["gt_trans"]),
+                     torch.from_numpy(np.stack(ref_L)), torch.from_numpy(b["gt_labels"]))
+    assert torch.equal(ours[:, 0], ref[:, 0]), (ours[:, 0].sum().item(), ref[:, 0].sum().item())
+    assert 0 < ours[:, 0].sum().item() < 64  # a regime where success is not trivial
 
 
 @pytest.mark.parametrize("scale,sigma", [(1e-3, 1e-4), (3.0, 0.1), (60.0, 1.2), (5e3, 37.0)])
@@ -291,11 +461,12 @@ def test_local_max_bit_exact_random(radius, gpu_device):
         assert np.array_equal(lm[b], O.local_max(src[b], conf[b], radius)), b
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("N", [300, 2000, 5000, 9000])  # 9000: rows past the register variants (R = 0)
-def test_seed_knn_random(N, gpu_device):
-    """a6 (split-fp16 distances + register radix select) against the oracle's
-    fp32 restatement, up to near-ties (assert_knn_equivalent); duplicate rows
-    make exact distance ties that must resolve by ascending index."""
+def test_seed_knn_random(N, precision, gpu_device):
+    """a6 (seed-row distances + register radix select) against the oracle's fp32
+    restatement, up to near-ties (assert_knn_equivalent); duplicate rows make
+    exact distance ties that must resolve by ascending index."""
     from oracle import pdsc_oracle as O
     from pointdsc_amd import kernels
     rng = np.random.RandomState(N)
@@ -306,14 +477,14 @@ def test_seed_knn_random(N, gpu_device):
     seeds = rng.choice(N, S, replace=False).astype(np.int32)
     seeds[0] = 40
     k = 40
-    knn = kernels.seed_knn(_t(f, gpu_device), _t(seeds[None], gpu_device, torch.int32), k)[0].cpu().numpy()
+    knn = kernels.seed_knn(_t(f, gpu_device), _t(seeds[None], gpu_device, torch.int32), k,
+                           precision=precision)[0].cpu().numpy()
     ref = O.knn_seed_rows(f[0], seeds.astype(np.int64), k)
     assert_knn_equivalent(knn, ref, f[0], seeds)
     # the tie group of seed 40 (rows 40, 50..59 identical): ascending index after the dropped first
     assert list(knn[0][:10]) == list(ref[0][:10])
 
 
-@pytest.mark.gpu
 @pytest.mark.parametrize("k,dups", [(40, 0), (63, 0), (63, 300), (40, 300), (8, 2)])
 def test_seed_knn_select_paths(k, dups, gpu_device):
     """knn_select's lane-minimum threshold fast path (want = k+1 <= 64, <= 128

@@ -5,12 +5,12 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import (assert_close_scaled, assert_knn_equivalent, assert_seeds_equivalent, golden_hparams, golden_names,
-                      golden_state_dict, load_golden)
+from conftest import (assert_close_scaled, assert_knn_equivalent, assert_rigid, assert_seeds_equivalent,
+                      assert_seeds_near_ties, golden_hparams, golden_names, golden_state_dict, load_golden, seed_H_rank)
 from oracle import pdsc_oracle as O
 
 NAMES = golden_names()
-FAST = [n for n in NAMES if not n.endswith("5k") and not n.endswith("5k_lo")]
+FAST = [n for n in NAMES if len(load_golden(n)["src_keypts"]) <= 1000]
 
 
 def _digest(sd):
@@ -72,10 +72,14 @@ def test_stages_isolated(name):
     ve = g["leading_eig"]
     w = (ve / (ve.sum(-1, keepdims=True) + np.float32(1e-6))).astype(np.float32)
     seed_trans = O.rigid_transform_3d(src[g["knn_idx"]], tgt[g["knn_idx"]], w)
-    np.testing.assert_allclose(seed_trans, g["seed_trans"], atol=1e-4)
+    ok = seed_H_rank(g) > 1e-5  # rank(H) < 2: the rotation is LAPACK's arbitrary pick (properties only)
+    np.testing.assert_allclose(seed_trans[ok], g["seed_trans"][ok], atol=1e-4)
+    for s in np.nonzero(~ok)[0]:
+        assert_rigid(seed_trans[s], src[g["knn_idx"][s]].astype(np.float64), tgt[g["knn_idx"][s]].astype(np.float64),
+                     w[s])
     # a10 from the reference hypotheses
     fitness, best, labels = O.verify(g["seed_trans"], src, tgt, tau)
-    assert np.array_equal(fitness, g["seed_fitness"])
+    assert np.array_equal(fitness, g["seed_fitness"])  # from the reference's own hypotheses: all seeds
     np.testing.assert_allclose(g["seed_trans"][best], g["trans_pre_refine"], atol=0)
     assert np.array_equal(labels, g["final_labels"])
     # a11 from the reference pre-refinement pose
@@ -99,10 +103,10 @@ def test_forward_5k(name):
     g = load_golden(name)
     out = O.forward_testing(g["corr_pos"], g["src_keypts"], g["tgt_keypts"], golden_state_dict(g),
                             record=True, **golden_hparams(g))
-    np.testing.assert_allclose(out["confidence"], g["confidence"], rtol=1e-5, atol=1e-3)
-    # seeds from our own confidences: NMS flips between neighbours whose scores
-    # differ by less than the fp32 error are legitimate; require >= 98 % overlap
-    assert len(set(out["seeds"].tolist()) & set(g["seeds"].tolist())) >= 0.98 * len(g["seeds"])
+    tol = float(np.abs(out["confidence"] - g["confidence"]).max())
+    assert tol <= 1e-3
+    # seeds from our own confidences: only near-tie decisions may differ (conftest)
+    assert_seeds_near_ties(out["seeds"], out["confidence"], g, tol)
     assert np.array_equal(out["final_labels"], g["final_labels"])
     np.testing.assert_allclose(out["final_trans"], g["final_trans"], atol=1e-4)
 

@@ -38,7 +38,30 @@ CASES = {
     "rel_5k":       (12, 5000, "3dmatch", 23, 0.3, False, False),
     "rel_5k_lo":    (12, 5000, "3dmatch", 24, 0.06, False, False),  # FPFH-like inlier ratio
     "rel_5k_kitti": (12, 5000, "kitti", 26, 0.3, False, False),     # BASELINE configs[4] shape
+    # rank-deficient neighbourhoods: 60 copies of one inlier correspondence and
+    # 60 collinear inliers (rigid_transform_3d's H of rank 0 / 1, common.py:7-45)
+    "degen_1k":     (12, 1000, "3dmatch", 27, 0.3, False, False),
+    "out_5k":       (12, 5000, "3dmatch", 28, 0.0, False, False),   # all outliers at full size
+    # evaluation/test_KITTI.py:151 builds up to num_node=12000 correspondences
+    "kitti_12k":    (12, 12000, "kitti", 29, 0.3, False, False),
 }
+
+# cases whose inputs are edited after synthetic_pair (name -> function(pair) -> pair)
+def _degenerate(pair):
+    src, tgt, gt = pair["src_keypts"].copy(), pair["tgt_keypts"].copy(), pair["gt_trans"].astype(np.float64)
+    inl = np.nonzero(pair["gt_labels"] > 0)[0]
+    dup, line = inl[1:61], inl[61:121]
+    src[dup], tgt[dup] = src[inl[0]], tgt[inl[0]]                  # duplicates of inlier inl[0]
+    p0, d = src[inl[0]].astype(np.float64), np.array([0.6, -0.3, 0.74])
+    pts = p0 + np.linspace(-0.8, 0.8, len(line))[:, None] * d / np.linalg.norm(d)
+    src[line] = pts.astype(np.float32)                             # collinear inliers
+    tgt[line] = (pts @ gt[:3, :3].T + gt[:3, 3]).astype(np.float32)
+    corr = np.concatenate([src, tgt], axis=-1)
+    return dict(pair, src_keypts=src, tgt_keypts=tgt, corr_pos=(corr - corr.mean(0)).astype(np.float32))
+
+
+MUTATE = {"degen_1k": _degenerate}
+STORE_FEATURES_MAX_N = 5000  # larger cases keep the logits, not the [N, 128] features
 
 
 def weights_digest(sd):
@@ -56,9 +79,11 @@ def run_case(name):
     sys.path.insert(0, REF)
     import models.PointDSC as refmod
 
-    torch.set_num_threads(1)
+    torch.set_num_threads(1 if N <= 5000 else os.cpu_count())
     p = PRESETS[preset]
     pair = synthetic_pair(N, pseed, preset, ratio)
+    if name in MUTATE:
+        pair = MUTATE[name](pair)
     sd_np = trained_state_dict(preset, L)
     # ctor exactly as evaluation/test_3DMatch.py:215-224 / test_KITTI.py:280-290
     model = refmod.PointDSC(in_dim=6, num_layers=L, num_channels=C, num_iterations=10,
@@ -138,7 +163,7 @@ def run_case(name):
         sigma_d=p["sigma_d"], inlier_threshold=p["inlier_threshold"], nms_radius=p["nms_radius"],
         corr_pos=pair["corr_pos"], src_keypts=pair["src_keypts"], tgt_keypts=pair["tgt_keypts"],
         gt_trans=pair["gt_trans"], gt_labels=pair["gt_labels"],
-        corr_features=rec["enc"][0].numpy().T.copy(),          # [N, C]
+        corr_features=rec["enc"][0].numpy().T.copy() if N <= STORE_FEATURES_MAX_N else np.zeros((0, C), np.float32),
         confidence=rec["conf"][0, 0].numpy(),                   # [N]
         is_local_max=rec["is_local_max"].numpy(),               # [N]
         seeds=seeds,                                            # [S]
@@ -168,7 +193,52 @@ def run_case(name):
           f"({os.path.getsize(path) / 1e3:.0f} kB)")
 
 
+def run_kabsch():
+    """The reference's rigid_transform_3d (models/common.py:7-45, LAPACK SVD on the
+    CPU) on degenerate inputs: all-zero and negative weights (H = 0: LAPACK's
+    U = V = I, so R = I), three points, coplanar points (rank-2 H: R unique),
+    and rank-1 H (collinear or duplicated points: R is LAPACK's choice among a
+    one-parameter family -- recorded, compared by properties only)."""
+    import torch
+    sys.path.insert(0, REF)
+    from models.common import rigid_transform_3d
+    rng = np.random.RandomState(31)
+    from pointdsc_amd.synthetic import random_rotation
+    cases = {}
+
+    def add(name, A, w, kind):
+        R = random_rotation(rng)
+        B = (A.astype(np.float64) @ R.T + rng.uniform(-1, 1, 3)).astype(np.float32)
+        with torch.no_grad():
+            T = rigid_transform_3d(torch.from_numpy(A)[None], torch.from_numpy(B)[None],
+                                   torch.from_numpy(w)[None]).numpy()[0]
+        cases[name] = (A, B, w, T, kind)
+
+    n = 40
+    A = rng.rand(n, 3).astype(np.float32)
+    add("zero_weights", A, np.zeros(n, np.float32), "pinned")
+    add("negative_weights", A, -rng.rand(n).astype(np.float32), "pinned")
+    add("three_points", rng.rand(3, 3).astype(np.float32), rng.rand(3).astype(np.float32), "pinned")
+    P = rng.rand(n, 3).astype(np.float32)
+    P[:, 2] = 0.5
+    add("coplanar", P, rng.rand(n).astype(np.float32), "pinned")
+    L = (rng.rand(1, 3) + np.linspace(0, 1, n)[:, None] * np.array([[0.3, -0.5, 0.8]])).astype(np.float32)
+    add("collinear", L, rng.rand(n).astype(np.float32), "properties")
+    D = np.repeat(rng.rand(1, 3), n, axis=0).astype(np.float32)
+    add("duplicates", D, rng.rand(n).astype(np.float32), "properties")
+    out = {}
+    for i, (k, (A, B, w, T, kind)) in enumerate(cases.items()):
+        out[f"{k}__A"], out[f"{k}__B"], out[f"{k}__w"], out[f"{k}__T"] = A, B, w, T
+        out[f"{k}__pinned"] = np.array(kind == "pinned")
+    path = os.path.join(REPO, "tests", "golden", "kabsch_degenerate.npz")
+    np.savez_compressed(path, **out)
+    print(f"kabsch_degenerate: {len(cases)} cases -> {os.path.relpath(path, REPO)}")
+
+
 if __name__ == "__main__":
-    names = sys.argv[1:] or list(CASES)
+    names = sys.argv[1:] or list(CASES) + ["kabsch"]
     for n in names:
-        run_case(n)
+        if n == "kabsch":
+            run_kabsch()
+        else:
+            run_case(n)
