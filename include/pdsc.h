@@ -228,6 +228,29 @@ int32_t pdsc_spectral_matching(const float *corr_pos, const float *src, const fl
  * measurement): y [N] = M [N,N] v [N].                                       */
 int32_t pdsc_sm_matvec(const float *M, const float *v, int32_t N, float *y, pdsc_stream_t stream);
 
+/* ------------------------------ f3 training-mode forward and loss ---------
+ * PointDSC.forward(data) WITHOUT the 'testing' key (models/PointDSC.py:158-163,
+ * 176, 182, 189-191) for B pairs (the training batch; forward only -- no
+ * gradients): M = clamp(1 - (1 - F^ F^T) / sigma^2, 0, 1) with a zero diagonal
+ * into M_out [B,N,N] (may be NULL), seeds = the int(N * ratio) largest logits
+ * (argsort, no NMS; ties by ascending index), seed hypotheses and verification
+ * as in testing, no post-refinement.  Outputs final_trans [B,4,4] and
+ * confidence [B,N] (the logits the reference returns as 'final_labels');
+ * seeds_out [B,int(N*ratio)] (may be NULL) receives the seed indices.       */
+size_t pdsc_forward_training_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N);
+int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                              const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
+                              float *confidence, float *M_out, int32_t *seeds_out, void *workspace,
+                              size_t workspace_bytes, pdsc_stream_t stream);
+/* SpectralMatchingLoss (libs/loss.py:115-139) of M [B,N,N] against gt_labels
+ * [B,N] (0/1): balanced != 0 -> mean over pairs of 0.5 sum gt (M-1)^2 /
+ * (relu(sum gt - 1) + 1) + 0.5 sum (1-gt) M^2 / (relu(sum (1-gt) - 1) + 1), else
+ * mean((M - gt)^2); gt_ij = (l_i + l_j == 2), gt_ii = 0.  Sums in fp64;
+ * loss: one device float.                                                   */
+size_t pdsc_spectral_matching_loss_workspace_bytes(int32_t B, int32_t N);
+int32_t pdsc_spectral_matching_loss(const float *M, const float *gt_labels, int32_t B, int32_t N, int32_t balanced,
+                                    float *loss, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
+
 /* ---------------------------------- f1 correspondence construction --------
  * Mutual nearest neighbours in descriptor space and the network inputs built
  * from them: replaces datasets/ThreeDMatch.py:277-308 (3DMatch / 3DLoMatch

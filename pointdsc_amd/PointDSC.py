@@ -12,11 +12,15 @@ demo_registration.py:78-88, evaluation/test_KITTI.py:280-293)::
     model = model.cuda().eval()
     res = model({'corr_pos': ..., 'src_keypts': ..., 'tgt_keypts': ..., 'testing': True})
 
-Scope: the testing path (``'testing' in data``) only.  The training forward
-(N x N feature-similarity M for the loss, autograd through SVD) is out of scope
-for this build and raises ``NotImplementedError``; the sub-modules exist only to
-hold the reference's parameters (their own ``forward`` raises as well) -- the
-encoder runs fused inside the kernels.
+Scope: the testing path (``'testing' in data``) and the training branch's
+evaluation-mode forward (no 'testing' key under ``model.eval()``: the
+validation loop of libs/trainer.py:202-239 -- final_trans, the logits as
+final_labels, and the N x N feature-similarity M its SpectralMatchingLoss
+consumes).  Training proper (BatchNorm batch statistics in ``model.train()``,
+autograd through the encoder and the SVD) is out of scope and raises
+``NotImplementedError``; the sub-modules exist only to hold the reference's
+parameters (their own ``forward`` raises as well) -- the encoder runs fused
+inside the kernels.
 """
 from __future__ import annotations
 
@@ -122,11 +126,18 @@ class PointDSC(nn.Module):
 
     # --------------------------------------------------------------- forward
     def forward(self, data):
-        """models/PointDSC.py:128-197 (testing mode; bs must be 1 as in :210/:414)."""
-        if "testing" not in data.keys():
-            raise NotImplementedError("training-mode forward (no 'testing' key) is out of scope for the "
-                                      "MI355X build; see DESIGN.md")
+        """models/PointDSC.py:128-197.  Testing mode: bs must be 1 as in :210/:414.
+        Without 'testing' (eval mode only, any bs): {final_trans, final_labels =
+        the logits, M = the feature-similarity matrix} (:158-163, :176-191)."""
         corr_pos, src, tgt = data["corr_pos"], data["src_keypts"], data["tgt_keypts"]
+        if "testing" not in data.keys():
+            if self.training:
+                raise NotImplementedError(
+                    "training-mode forward in model.train() (BatchNorm batch statistics, autograd) is out of "
+                    "scope for the MI355X build; call model.eval() for the validation forward (DESIGN.md)")
+            trans, conf, M, _ = kernels.forward_training(self.pdsc_config(), self.packed_weights(), corr_pos, src,
+                                                         tgt)
+            return {"final_trans": trans, "final_labels": conf, "M": M}
         assert corr_pos.shape[0] == 1  # pick_seeds / post_refinement support bs = 1 only
         trans, labels = kernels.forward_testing(self.pdsc_config(), self.packed_weights(), corr_pos, src, tgt)
         return {"final_trans": trans, "final_labels": labels, "M": None}

@@ -88,6 +88,10 @@ _PROTOS = {
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
                                        c_size_t, vp]),
+    "pdsc_forward_training_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
+    "pdsc_forward_training": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_spectral_matching_loss_workspace_bytes": (c_size_t, [c_int32, c_int32]),
+    "pdsc_spectral_matching_loss": (c_int32, [vp, vp, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
 }
 
 EXPORTS = tuple(_PROTOS)

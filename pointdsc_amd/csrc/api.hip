@@ -601,6 +601,71 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
 }
 
 
+// ------------------------------------------- f3 training-mode forward and loss
+size_t pdsc_forward_training_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N) {
+    return pdsc_forward_workspace_bytes(cfg, B, N);
+}
+
+int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const float *corr_pos, const float *src,
+                              const float *tgt, int32_t B, int32_t N, float *final_trans, float *confidence,
+                              float *M_out, int32_t *seeds_out, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cfg(cfg));
+    Dims d;
+    RET_IF(make_dims(cfg, B, N, d));
+    if (!packed || !corr_pos || !src || !tgt || !final_trans || !confidence || !ws)
+        return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_forward_training_workspace_bytes(cfg, B, N)));
+    hipStream_t s = S_(stream);
+    Carve c(ws);
+    const FwdBufs f = carve_forward(c, d);
+    const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
+    const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
+    // a1-a4 as in testing (:150-156, :171)
+    const bool mpacked = !dense_m_requested() && !d.f32;
+    if (mpacked)
+        HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    else
+        HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
+    // the loss's feature-similarity M (:158-163)
+    if (M_out)
+        HIPCHK(launch_feat_sim(d.f32 ? static_cast<const void *>(f.normed) : static_cast<const void *>(f.normed_s),
+                               d.f32, d.B, d.N, sigma, M_out, s));
+    // seeds = argsort(confidence, descending)[:, :S] (:176): the ranking with every flag 1
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(f.lm), 0x3f800000u, (size_t)d.B * d.N, s));
+    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
+    // a6-a10 as in testing (:182 -> cal_seed_trans), no post-refinement (:185-186)
+    HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
+    if (d.f32)
+        HIPCHK(launch_knn_dist_f32(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    else
+        HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
+    HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
+    RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm,
+                   f.weights, nullptr, s));
+    HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold, f.seed_trans,
+                             f.counts, f.hsums, s));
+    // the labels of the best hypothesis are not returned in training mode (:189-191): f.lm is scratch
+    HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold, nullptr,
+                              nullptr, final_trans, f.lm, s));
+    HIPCHK(hipMemcpyAsync(confidence, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
+    if (seeds_out) HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    return PDSC_OK;
+}
+
+size_t pdsc_spectral_matching_loss_workspace_bytes(int32_t B, int32_t N) {
+    return (B < 1 || N < 1) ? 0 : align_bytes(sm_loss_partial_doubles(B, N) * sizeof(double));
+}
+
+int32_t pdsc_spectral_matching_loss(const float *M, const float *gt_labels, int32_t B, int32_t N, int32_t balanced,
+                                    float *loss, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    if (!M || !gt_labels || !loss || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    RET_IF(need_ws(ws_bytes, pdsc_spectral_matching_loss_workspace_bytes(B, N)));
+    HIPCHK(launch_sm_loss(M, gt_labels, B, N, balanced, static_cast<double *>(ws), loss, S_(stream)));
+    return PDSC_OK;
+}
+
 // ------------------------------------------------- f1 correspondence construction
 size_t pdsc_mutual_nn_workspace_bytes(int32_t Ns, int32_t Nt) {
     return align_bytes((size_t)Ns * 8) + align_bytes((size_t)Nt * 8);

@@ -55,12 +55,14 @@ __global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w
 }
 
 // W [out][in] (torch Conv1d weight) -> three fp16 planes hi, mid, lo of
-// W * 2^s = hi + mid + lo (33 significant bits: every fp32 weight exactly),
-// each [out][in] with the inputs of every 16-wide k-step in qk_pos order
-// (bits 2 and 3 of the index swapped): lane (h, n) of a 32x32x16 MFMA reads
-// positions 8h .. 8h+7 of output n as one 16-B load -- inputs {4h..4h+3,
+// W * 2^s = hi + mid + lo (33 significant bits: every fp32 weight exactly) in
+// MFMA-fragment blocks (w3_index, pdsc_internal.hpp): block (t, ks) = outputs
+// 32t..32t+31 x the 16 inputs of k-step ks, planes hi / mid / lo of 1 KiB
+// each, lane (h, n)'s 16 B = positions 8h .. 8h+7 of output 32t + n in qk_pos
+// order (bits 2 and 3 of the input index swapped: inputs {4h..4h+3,
 // 8+4h..8+4h+3} of the k-step, exactly the channels a transposed product's
-// accumulator half h holds (f32: W itself, fp32 [out][in], natural order).
+// accumulator half h holds).  Blocks are stored t-major, so any run of
+// consecutive blocks is one contiguous copy (f32: W itself, fp32 [out][in]).
 // BN folded as torch-CPU eval folds it.
 __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__restrict__ b,
                                   const float *__restrict__ bn_w, const float *__restrict__ bn_b,
@@ -73,16 +75,16 @@ __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__re
     if (i < total && f32) {
         dw[i] = w[i];
     } else if (i < total) {
-        _Float16 *wh = reinterpret_cast<_Float16 *>(dw), *wm = wh + total, *wl = wm + total;
+        _Float16 *wd = reinterpret_cast<_Float16 *>(dw);
         const int o = i / in, c = i % in;
-        const int d = o * in + qk_pos(c);
         const float x = w[i] * sc[1];  // exact (power of two)
         const _Float16 hi = (_Float16)x;
         const float r1 = x - (float)hi;  // exact
         const _Float16 mid = (_Float16)r1;
-        wh[d] = hi;
-        wm[d] = mid;
-        wl[d] = (_Float16)(r1 - (float)mid);
+        const size_t d = w3_index(o, c, in);
+        wd[d] = hi;
+        wd[d + 512] = mid;
+        wd[d + 1024] = (_Float16)(r1 - (float)mid);
     }
     if (i < out) {
         db[i] = b[i];
@@ -268,14 +270,12 @@ PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int
 #pragma unroll
         for (int j = 0; j < IN / 8; ++j) p.w[j] = *reinterpret_cast<const f32x4 *>(W + rowo + 8 * j);
     } else {
-        const _Float16 *Wh = reinterpret_cast<const _Float16 *>(pk + off.w);
-        const _Float16 *Wm = Wh + (size_t)OUT * IN, *Wl = Wm + (size_t)OUT * IN;
-        const size_t rowo = (size_t)(ct * 32 + (lane & 31)) * IN + 8 * (lane >> 5);
+        const _Float16 *W = reinterpret_cast<const _Float16 *>(pk + off.w) + (size_t)ct * (IN / 16) * W3_BLOCK + 8 * lane;
 #pragma unroll
         for (int ks = 0; ks < IN / 16; ++ks) {
-            p.h[ks] = *reinterpret_cast<const f16x8 *>(Wh + rowo + 16 * ks);
-            p.m[ks] = *reinterpret_cast<const f16x8 *>(Wm + rowo + 16 * ks);
-            p.l[ks] = *reinterpret_cast<const f16x8 *>(Wl + rowo + 16 * ks);
+            p.h[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK);
+            p.m[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK + 512);
+            p.l[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK + 1024);
         }
     }
 }
@@ -726,92 +726,65 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 // with no data movement between lanes.  V runs untransposed (A = activations,
 // B = weights) to come out in the attention's V-tile layout.
 //
-// Weights: blocks (one 32-output tile x one 16-input k-step: hi, mid, lo
-// planes, 1 KiB each) copied into LDS by LDS-DMA, PW2_CB blocks per chunk,
-// double-buffered and shared by the workgroup's waves; the chunk after the one
-// being multiplied is in flight meanwhile.  Per-channel epilogue coefficients
-// (bias, BN alpha / beta) of every layer of the kernel sit in LDS for the
-// whole launch.  Two workgroups per CU (~53 KiB of LDS and <= 256 VGPRs each)
-// overlap one's HBM phases with the other's MFMAs.
-//
-// Barriers: each chunk ends with "s_waitcnt vmcnt(n); s_barrier" where n
-// counts only the global stores issued after that chunk's DMA -- a layer's
-// output stores are issued by the NEXT layer right after it has queued its
-// first DMA (the `pre` hook), so no barrier waits on a store.
+// Weights: the kernel's layers are cut into chunks of <= PW2_CB weight blocks
+// (w3_index: one block = 32 outputs x 16 inputs x 3 planes = 3 KiB,
+// contiguous per chunk), listed in consumption order by the host (W2Sched).
+// Chunks are copied into a 2-slot LDS ring by LDS-DMA and shared by the
+// workgroup's waves: right after the barrier that retires chunk c, chunk c + 2
+// is queued into the slot c just freed -- before any epilogue work -- so the
+// barrier at the end of chunk c + 1 waits only for that DMA (vmcnt counts the
+// epilogue's later stores out), and no store is ever waited for.  Per-channel
+// epilogue coefficients (bias, BN alpha / beta) sit in LDS for the launch.
+// Two workgroups per CU (~55 KiB of LDS and <= 256 VGPRs each) overlap one's
+// HBM phases and epilogues with the other's MFMAs.
 constexpr int PW2_W = 4;                              // waves per workgroup: 128 points
 constexpr int PW2_CB = 8;                             // blocks per chunk (24 KiB)
 constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 planes)
+constexpr int PW2_SLOT = PW2_CB * PW2_BLKB;
 constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
-constexpr size_t PW2_LDS = 2 * PW2_CB * PW2_BLKB + PW2_COEF * sizeof(float);
+constexpr size_t PW2_LDS = 2 * PW2_SLOT + PW2_COEF * sizeof(float);
+constexpr int W2_MAXCH = 24;
 
-struct W2Chunk {  // blocks (t, ks), t in [t0, t0 + nt), ks in [0, in / 16), of one packed layer
-    const _Float16 *w;
-    int in, out, t0, nt;
+struct W2Sched {                 // chunk c: np[c] pieces of 1 KiB starting at pk-halfs off[c]
+    uint32_t off[W2_MAXCH];
+    int32_t np[W2_MAXCH];
+    int32_t n;
 };
 
-PDSC_DEV W2Chunk w2_chunk(const float *pk, const DenseOff &o, int in, int out, int t0, int nt) {
-    return W2Chunk{reinterpret_cast<const _Float16 *>(pk + o.w), in, out, t0, nt};
-}
 // output tiles per chunk of an IN -> OUT layer
 constexpr int w2_nt(int in, int out) {
     return PW2_CB / (in / 16) < 1 ? 1 : (PW2_CB / (in / 16) < out / 32 ? PW2_CB / (in / 16) : out / 32);
 }
 
-// LDS-DMA of one chunk: piece (blk, plane) = 1 KiB = one wave instruction, lane
-// (h, n) fetching inputs 8h .. 8h+7 of output 32 t + n -- the reader's lane
-// reads the same 16 B back at 16 * lane (lane-linear, conflict-free).
-PDSC_DEV void w2_stage(const W2Chunk &c, char *slot, int wave, int lane) {
-    const int nks = c.in / 16, npieces = c.nt * nks * 3;
-    const size_t plane_sz = (size_t)c.out * c.in;
-    const _Float16 *base = c.w + (size_t)(32 * c.t0 + (lane & 31)) * c.in + 8 * (lane >> 5);
-    for (int i = wave; i < npieces; i += PW2_W) {
-        const int blk = i / 3, plane = i - 3 * blk;
-        const int t = blk / nks, ks = blk - t * nks;
-        __builtin_amdgcn_global_load_lds(base + plane * plane_sz + (size_t)(32 * t) * c.in + 16 * ks,
-                                         slot + (blk * 3 + plane) * 1024, 16, 0, 0);
+// Host: append a layer's chunks to the schedule (same cut as w2_layer).
+static void w2_sched_add(W2Sched &S, const DenseOff &o, int in, int out) {
+    const int nks = in / 16, nt = w2_nt(in, out);
+    for (int c = 0; c < out / 32 / nt; ++c) {
+        S.off[S.n] = (uint32_t)(2 * o.w + (size_t)c * nt * nks * W3_BLOCK);
+        S.np[S.n] = 3 * nt * nks;
+        ++S.n;
     }
 }
 
-// acc[t0 + t] += W_t X for the chunk's NT tiles x NKS k-steps (TRANS: A = W, B =
-// X); the fragments of block j + 1 are read while block j's MFMAs run, and the
-// empty asm keeps the compiler from hoisting further reads (registers).
-template <int NKS, int NT, bool TRANS, int NACC>
-PDSC_DEV void w2_mma(const char *slot, const f16x8 *xh, const f16x8 *xl, f32x16 (&acc)[NACC], int t0, int lane) {
-    const char *bp = slot + 16 * lane;
-    f16x8 w0 = *reinterpret_cast<const f16x8 *>(bp), w1 = *reinterpret_cast<const f16x8 *>(bp + 1024),
-          w2 = *reinterpret_cast<const f16x8 *>(bp + 2048);
-#pragma unroll
-    for (int j = 0; j < NT * NKS; ++j) {
-        const int t = j / NKS, ks = j % NKS;
-        f16x8 n0 = w0, n1 = w1, n2 = w2;
-        if (j + 1 < NT * NKS) {
-            const char *np = bp + (j + 1) * PW2_BLKB;
-            n0 = *reinterpret_cast<const f16x8 *>(np);
-            n1 = *reinterpret_cast<const f16x8 *>(np + 1024);
-            n2 = *reinterpret_cast<const f16x8 *>(np + 2048);
-        }
-        acc[t0 + t] = TRANS ? mfma_w3x(w0, w1, w2, xh[ks], xl[ks], acc[t0 + t])
-                            : mfma_xw3(xh[ks], xl[ks], w0, w1, w2, acc[t0 + t]);
-        asm volatile("" ::: "memory");
-        w0 = n0;
-        w1 = n1;
-        w2 = n2;
-    }
+// LDS-DMA of chunk c into `slot` (nothing past the schedule): piece i = 1 KiB =
+// one wave instruction, lane-linear on both sides.
+PDSC_DEV void w2_stage(const float *pk, const W2Sched &S, int c, char *slot, int wave, int lane) {
+    if (c >= S.n) return;
+    const _Float16 *src = reinterpret_cast<const _Float16 *>(pk) + S.off[c] + 8 * lane;
+    for (int i = wave; i < S.np[c]; i += PW2_W)
+        __builtin_amdgcn_global_load_lds(src + 512 * i, slot + 1024 * i, 16, 0, 0);
 }
 
-struct W2Pipe {  // the two LDS slots; chunk c is multiplied from `cur` while c + 1 lands in `nxt`
-    char *cur, *nxt;
-    PDSC_DEV void swap() {
-        char *t = cur;
-        cur = nxt;
-        nxt = t;
-    }
+struct W2Pipe {
+    char *base;
+    int c;  // chunk being multiplied
+    PDSC_DEV char *slot(int k) const { return base + (k & 1) * PW2_SLOT; }
 };
 
-// End of a chunk: this wave's DMA pieces have landed (all but its `nst` youngest
-// vector-memory ops, the stores issued after them, are done) and its LDS reads
-// of the chunk have returned, then the barrier.
+// End of a chunk: this wave's DMA of the next chunk has landed (all but its
+// NST youngest vector-memory ops -- the stores issued after that DMA -- are
+// done) and its LDS reads have returned, then the barrier.
 template <int NST>
 PDSC_DEV void w2_sync(bool active) {
     if (NST > 0 && active)
@@ -820,37 +793,55 @@ PDSC_DEV void w2_sync(bool active) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-struct W2NoPre {
-    PDSC_DEV void operator()() const {}
-};
+PDSC_DEV void w2_frag(const char *bp, f16x8 (&w)[3]) {
+    w[0] = *reinterpret_cast<const f16x8 *>(bp);
+    w[1] = *reinterpret_cast<const f16x8 *>(bp + 1024);
+    w[2] = *reinterpret_cast<const f16x8 *>(bp + 2048);
+}
 
-// One dense layer IN -> OUT: per chunk, queue the next chunk (or `after`, the
-// next layer's first), run `pre` once (the previous layer's NST stores), multiply,
-// sync.  P.cur must hold this layer's first chunk.
-template <int IN, int OUT, bool TRANS, int NST = 0, typename PRE = W2NoPre>
-PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const DenseOff &o, const W2Chunk *after, const f16x8 *xh,
-                       const f16x8 *xl, f32x16 (&acc)[OUT / 32], bool active, int wave, int lane,
-                       const PRE &pre = PRE()) {
+// acc[t0 + t] += W_t X over the chunk's NT tiles x NKS k-steps (TRANS: A = W,
+// B = X).  The fragments of block j + 2 are read while block j's MFMAs run (a
+// ring of three register sets with compile-time indices); sched_barrier(0)
+// pins that order (left alone, the scheduler sinks every read next to its
+// MFMA and exposes the LDS latency each time).
+template <int NKS, int NT, bool TRANS, int NACC>
+PDSC_DEV void w2_mma(const char *slot, const f16x8 *xh, const f16x8 *xl, f32x16 (&acc)[NACC], int t0, int lane) {
+    constexpr int NB = NT * NKS;
+    const char *bp = slot + 16 * lane;
+    f16x8 w[3][3];
+    w2_frag(bp, w[0]);
+    if (NB > 1) w2_frag(bp + PW2_BLKB, w[1]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        if (j + 2 < NB) w2_frag(bp + (j + 2) * PW2_BLKB, w[(j + 2) % 3]);
+        const int t = j / NKS, ks = j % NKS;
+        const f16x8(&f)[3] = w[j % 3];
+        acc[t0 + t] = TRANS ? mfma_w3x(f[0], f[1], f[2], xh[ks], xl[ks], acc[t0 + t])
+                            : mfma_xw3(xh[ks], xl[ks], f[0], f[1], f[2], acc[t0 + t]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// One dense layer IN -> OUT.  Per chunk: multiply, sync (NST: the stores the
+// caller issued since the previous barrier), queue chunk + 2 into the slot just
+// retired.
+template <int IN, int OUT, bool TRANS, int NST = 0>
+PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const W2Sched &S, const f16x8 *xh, const f16x8 *xl,
+                       f32x16 (&acc)[OUT / 32], bool active, int wave, int lane) {
     constexpr int NKS = IN / 16, NT = w2_nt(IN, OUT), NCH = OUT / 32 / NT;
     static_assert(NCH * NT == OUT / 32, "chunk tiling");
 #pragma unroll
     for (int t = 0; t < OUT / 32; ++t) acc[t] = zero16();
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        if (c + 1 < NCH)
-            w2_stage(w2_chunk(pk, o, IN, OUT, (c + 1) * NT, NT), P.nxt, wave, lane);
-        else if (after)
-            w2_stage(*after, P.nxt, wave, lane);
-        asm volatile("" ::: "memory");
-        if (c == 0) {
-            pre();
-            if (active) w2_mma<NKS, NT, TRANS>(P.cur, xh, xl, acc, 0, lane);
+        if (active) w2_mma<NKS, NT, TRANS>(P.slot(P.c), xh, xl, acc, c * NT, lane);
+        if (c == 0)
             w2_sync<NST>(active);
-        } else {
-            if (active) w2_mma<NKS, NT, TRANS>(P.cur, xh, xl, acc, c * NT, lane);
+        else
             w2_sync<0>(active);
-        }
-        P.swap();
+        w2_stage(pk, S, P.c + 2, P.slot(P.c), wave, lane);
+        asm volatile("" ::: "memory");
+        ++P.c;
     }
 }
 
@@ -1042,31 +1033,26 @@ PDSC_DEV void w2_coef_qkv(float *cf, const float *pk, const PwDense4 &d, int tid
 }
 
 // PointCN (BN, ReLU) of the fragments x, then the Q/K/V projections; the
-// PointCN rows go to featL.  Expects P.cur = the PCN layer's first chunk;
-// `pre` = the caller's pending stores (NST of them), issued in the PCN layer.
-template <int NST, typename PRE>
-PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const float *cf, const PwDense4 &d, const f16x8 *xh,
-                         const f16x8 *xl, float *__restrict__ featL, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                         _Float16 *__restrict__ V, float *__restrict__ vexp, int row, bool active, int wave, int lane,
-                         const PRE &pre) {
+// PointCN rows go to featL.  The pipeline is at the PointCN layer's first chunk.
+PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const W2Sched &S, const float *cf, const PwDense4 &d,
+                         const f16x8 *xh, const f16x8 *xl, float *__restrict__ featL, _Float16 *__restrict__ Q,
+                         _Float16 *__restrict__ K, _Float16 *__restrict__ V, float *__restrict__ vexp, int row,
+                         bool active, int wave, int lane) {
     const int h = lane >> 5;
-    f32x16 ap[4], aq[4];
+    f32x16 acc[4];
     f16x8 yh[8], yl[8];
-    const W2Chunk q0 = w2_chunk(pk, d.q, CH, CH, 0, w2_nt(CH, CH)), k0 = w2_chunk(pk, d.k, CH, CH, 0, w2_nt(CH, CH)),
-                  v0 = w2_chunk(pk, d.v, CH, CH, 0, w2_nt(CH, CH));
     const float sp = pk[d.pcn.scale], sq = pk[d.q.scale], sk = pk[d.k.scale], sv = pk[d.v.scale];
-    w2_layer<CH, CH, true, NST>(P, pk, d.pcn, &q0, xh, xl, ap, active, wave, lane, pre);
-    if (active) w2_epilogue<CH, EPI_BN_RELU>(ap, sp, cf + W2CoefQKV::pcn, nullptr, yh, yl, lane);
-    w2_layer<CH, CH, true, 16>(P, pk, d.q, &k0, yh, yl, aq, active, wave, lane, [&] {
-        if (active) w2_store_row(featL, row, h, ap);
-    });
-    w2_layer<CH, CH, true, 16>(P, pk, d.k, &v0, yh, yl, ap, active, wave, lane, [&] {
-        if (active) w2_store_qk<false>(aq, sq, cf + W2CoefQKV::q, Q, row, lane);
-    });
-    w2_layer<CH, CH, false, 16>(P, pk, d.v, nullptr, yh, yl, aq, active, wave, lane, [&] {
-        if (active) w2_store_qk<true>(ap, sk, cf + W2CoefQKV::k, K, row, lane);
-    });
-    if (active) w2_store_v(aq, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * (2 * CH * H3_TILE), vexp + (row >> 5), lane);
+    w2_layer<CH, CH, true>(P, pk, S, xh, xl, acc, active, wave, lane);
+    if (active) {
+        w2_epilogue<CH, EPI_BN_RELU>(acc, sp, cf + W2CoefQKV::pcn, nullptr, yh, yl, lane);
+        w2_store_row(featL, row, h, acc);
+    }
+    w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
+    if (active) w2_store_qk<false>(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
+    w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
+    if (active) w2_store_qk<true>(acc, sk, cf + W2CoefQKV::k, K, row, lane);
+    w2_layer<CH, CH, false, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
+    if (active) w2_store_v(acc, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * (2 * CH * H3_TILE), vexp + (row >> 5), lane);
 }
 
 #define PW2_PROLOGUE                                                                              \
@@ -1075,19 +1061,20 @@ PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const float *c
     const int row = blockIdx.x * PW2_PTS + wave * 32 + (lane & 31);                               \
     const bool active = blockIdx.x * PW2_PTS + wave * 32 < Npad; /* wave-uniform */               \
     const size_t boff = (size_t)b * Npad * CH;                                                    \
-    W2Pipe P{w2smem, w2smem + PW2_CB * PW2_BLKB};                                                 \
-    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_CB * PW2_BLKB);
+    W2Pipe P{w2smem, 0};                                                                          \
+    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);                                 \
+    w2_stage(pk, S, 0, P.slot(0), wave, lane);                                                    \
+    w2_stage(pk, S, 1, P.slot(1), wave, lane);
 
 // layer0 (Conv1d in_dim -> 128 on exact fp32 MFMA 32x32x2, k-step j: inputs 2j + h)
 // + PointCN_0 + QKV_0.
-__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *__restrict__ pk, size_t l0w, size_t l0b,
-                                                                 PwDense4 d, const float *__restrict__ corr, int in_dim,
-                                                                 int N, int Npad, float *__restrict__ featL,
+__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *__restrict__ pk, W2Sched S, size_t l0w,
+                                                                 size_t l0b, PwDense4 d, const float *__restrict__ corr,
+                                                                 int in_dim, int N, int Npad, float *__restrict__ featL,
                                                                  _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                                  _Float16 *__restrict__ V, float *__restrict__ vexp) {
     PW2_PROLOGUE
     const int l32 = lane & 31;
-    w2_stage(w2_chunk(pk, d.pcn, CH, CH, 0, w2_nt(CH, CH)), P.cur, wave, lane);
     w2_coef_qkv(cf, pk, d, tid);
     f16x8 xh[8], xl[8];
     if (active) {
@@ -1114,13 +1101,13 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *_
             }
     }
     __syncthreads();
-    w2_pcn_qkv<0>(P, pk, cf, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane, W2NoPre());
+    w2_pcn_qkv(P, pk, S, cf, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+               vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
 }
 
 // combine_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1}.
-__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
-                                                               const float *__restrict__ opart,
+__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
+                                                               PwDense4 d, const float *__restrict__ opart,
                                                                const float *__restrict__ ml, int nsplit, int N,
                                                                int Npad, float *__restrict__ featL,
                                                                _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
@@ -1128,7 +1115,6 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__r
     PW2_PROLOGUE
     constexpr int CF0 = W2CoefQKV::end, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2;
     static_assert(CF6 + 3 * CH <= PW2_COEF, "coefficient table");
-    w2_stage(w2_chunk(pk, m.fc0, CH, CH2, 0, w2_nt(CH, CH2)), P.cur, wave, lane);
     w2_coef_qkv(cf, pk, d, tid);
     w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
     w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
@@ -1136,26 +1122,24 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__r
     f16x8 xh[8], xl[8];
     if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
     __syncthreads();
-    const W2Chunk fc3 = w2_chunk(pk, m.fc3, CH2, CH2, 0, w2_nt(CH2, CH2)), fc6 = w2_chunk(pk, m.fc6, CH2, CH, 0, w2_nt(CH2, CH)),
-                  pcn = w2_chunk(pk, d.pcn, CH, CH, 0, w2_nt(CH, CH));
     f32x16 a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];
-    w2_layer<CH, CH2, true>(P, pk, m.fc0, &fc3, xh, xl, a2, active, wave, lane);
+    w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
     if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + CF0, nullptr, yh, yl, lane);
-    w2_layer<CH2, CH2, true>(P, pk, m.fc3, &fc6, yh, yl, a2, active, wave, lane);
+    w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
         w2_load_row(featL + boff, row, h, res);  // the residual: lands during fc6's MFMAs
     }
-    w2_layer<CH2, CH, true>(P, pk, m.fc6, &pcn, xh, xl, a4, active, wave, lane);
+    w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);
-    w2_pcn_qkv<0>(P, pk, cf, d, yh, yl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane, W2NoPre());
+    w2_pcn_qkv(P, pk, S, cf, d, yh, yl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+               vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
 }
 
 // combine + fc_message + residual, then F.normalize (:156) and the classifier (:171).
 __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
-    const float *__restrict__ pk, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
+    const float *__restrict__ pk, W2Sched S, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
     const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
     const float *__restrict__ featL, float *__restrict__ feat_out, float *__restrict__ normed,
     _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
@@ -1163,7 +1147,6 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
     constexpr int CF0 = 0, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2, CC0 = CF6 + 3 * CH, CC2 = CC0 + 3 * CLS,
                   CC4 = CC2 + 3 * CLS;
     static_assert(CC4 + CLS <= PW2_COEF, "coefficient table");
-    w2_stage(w2_chunk(pk, m.fc0, CH, CH2, 0, w2_nt(CH, CH2)), P.cur, wave, lane);
     w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
     w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
     w2_coef(cf + CF6, pk, m.fc6, CH, tid);
@@ -1173,20 +1156,17 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
     f16x8 xh[8], xl[8];
     if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
     __syncthreads();
-    const W2Chunk fc3 = w2_chunk(pk, m.fc3, CH2, CH2, 0, w2_nt(CH2, CH2)), fc6 = w2_chunk(pk, m.fc6, CH2, CH, 0, w2_nt(CH2, CH)),
-                  cc0 = w2_chunk(pk, c0, CH, CLS, 0, w2_nt(CH, CLS)), cc2 = w2_chunk(pk, c2, CLS, CLS, 0, w2_nt(CLS, CLS));
     f32x16 a1[1], a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];
-    w2_layer<CH, CH2, true>(P, pk, m.fc0, &fc3, xh, xl, a2, active, wave, lane);
+    w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
     if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + CF0, nullptr, yh, yl, lane);
-    w2_layer<CH2, CH2, true>(P, pk, m.fc3, &fc6, yh, yl, a2, active, wave, lane);
+    w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
         w2_load_row(featL + boff, row, h, res);
     }
-    w2_layer<CH2, CH, true>(P, pk, m.fc6, &cc0, xh, xl, a4, active, wave, lane);
+    w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     const bool in = row < N;
-    float den = 1.0f;
     if (active) {
         w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);  // a4 = corr_features (:155)
         float ss = 0.0f;  // F.normalize(p=2, dim=-1, eps=1e-12) (:156)
@@ -1195,43 +1175,42 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) ss = __builtin_fmaf(a4[t][r], a4[t][r], ss);
         ss += __shfl_xor(ss, 32);
-        den = fmaxf(sqrtf(ss), 1e-12f);
-    }
-    // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171);
-    // the feature / normed stores are issued inside the first classifier layer
-    w2_layer<CH, CLS, true, 32>(P, pk, c0, &cc2, yh, yl, a1, active, wave, lane, [&] {
-        if (!active || !in) return;
-        float *dst = normed + ((size_t)b * N + row) * CH;
-        _Float16 *ds = normed_s ? normed_s + ((size_t)b * N + row) * 2 * CH : nullptr;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = a4[t][8 * u + e] / den;
-                *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 4 * h) = f32x4{v[0], v[1], v[2], v[3]};
-                *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 8 + 4 * h) = f32x4{v[4], v[5], v[6], v[7]};
-                if (ds) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
-                    f16x8 hi, lo;
-                    split8v(v, hi, lo);
-                    const int chk = 4 * t + 2 * u + h;
-                    *reinterpret_cast<f16x8 *>(ds + 8 * chk) = hi;
-                    *reinterpret_cast<f16x8 *>(ds + CH + 8 * chk) = lo;
-                }
-            }
-        if (feat_out) {  // natural channel order (the standalone encoder API only)
-            float *fo = feat_out + ((size_t)b * N + row) * CH;
+        const float den = fmaxf(sqrtf(ss), 1e-12f);
+        if (in) {
+            float *dst = normed + ((size_t)b * N + row) * CH;
+            _Float16 *ds = normed_s ? normed_s + ((size_t)b * N + row) * 2 * CH : nullptr;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<f32x4 *>(fo + 32 * t + 8 * g + 4 * h) =
-                        f32x4{a4[t][4 * g], a4[t][4 * g + 1], a4[t][4 * g + 2], a4[t][4 * g + 3]};
+                for (int u = 0; u < 2; ++u) {
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = a4[t][8 * u + e] / den;
+                    *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 4 * h) = f32x4{v[0], v[1], v[2], v[3]};
+                    *reinterpret_cast<f32x4 *>(dst + 32 * t + 16 * u + 8 + 4 * h) = f32x4{v[4], v[5], v[6], v[7]};
+                    if (ds) {  // the fp16 hi/lo split copy (qk_pos order) the seed kNN consumes
+                        f16x8 hi, lo;
+                        split8v(v, hi, lo);
+                        const int chk = 4 * t + 2 * u + h;
+                        *reinterpret_cast<f16x8 *>(ds + 8 * chk) = hi;
+                        *reinterpret_cast<f16x8 *>(ds + CH + 8 * chk) = lo;
+                    }
+                }
+            if (feat_out) {  // natural channel order (the standalone encoder API only)
+                float *fo = feat_out + ((size_t)b * N + row) * CH;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *reinterpret_cast<f32x4 *>(fo + 32 * t + 8 * g + 4 * h) =
+                            f32x4{a4[t][4 * g], a4[t][4 * g + 1], a4[t][4 * g + 2], a4[t][4 * g + 3]};
+            }
         }
-    });
+    }
+    // classification MLP 128 -> 32 -> 32 -> 1 on the unnormalised features (:171)
+    w2_layer<CH, CLS, true>(P, pk, S, yh, yl, a1, active, wave, lane);
     if (active) w2_epilogue<CLS, EPI_RELU>(a1, pk[c0.scale], cf + CC0, nullptr, xh, xl, lane);
-    w2_layer<CLS, CLS, true>(P, pk, c2, nullptr, xh, xl, a1, active, wave, lane);
+    w2_layer<CLS, CLS, true>(P, pk, S, xh, xl, a1, active, wave, lane);
     if (active) {
         w2_epilogue<CLS, EPI_RELU, false>(a1, pk[c2.scale], cf + CC2, nullptr, nullptr, nullptr, lane);
         float s = 0.0f;  // this half's 16 channels, then the other half's
@@ -1254,6 +1233,21 @@ static bool use_pw2(int B, int Npad, bool f32) {
     }();
     if (f32 || mode == 0) return false;
     return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) >= 512;
+}
+
+static W2Sched sched_qkv(W2Sched S, const PwDense4 &d) {
+    w2_sched_add(S, d.pcn, CH, CH);
+    w2_sched_add(S, d.q, CH, CH);
+    w2_sched_add(S, d.k, CH, CH);
+    w2_sched_add(S, d.v, CH, CH);
+    return S;
+}
+static W2Sched sched_msg(const PwMsg &m) {
+    W2Sched S{};
+    w2_sched_add(S, m.fc0, CH, CH2);
+    w2_sched_add(S, m.fc3, CH2, CH2);
+    w2_sched_add(S, m.fc6, CH2, CH);
+    return S;
 }
 
 static PwDense4 dense4(const LayerOff &l) { return PwDense4{l.pcn, l.q, l.k, l.v}; }
@@ -1291,8 +1285,9 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
+        const W2Sched S = sched_qkv(W2Sched{}, dense4(lay.layer[0]));
         hipLaunchKernelGGL(pw2_first_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
-                           packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K,
+                           packed, S, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K,
                            V, vexp);
         return hipGetLastError();
     }
@@ -1306,8 +1301,9 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
                          float *vexp, hipStream_t s) {
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
+        const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
         hipLaunchKernelGGL(pw2_mid_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
-                           packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad,
+                           packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad,
                            feat, Q, K, V, vexp);
         return hipGetLastError();
     }
@@ -1320,8 +1316,11 @@ hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, 
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s) {
     if (use_pw2(B, Npad, f32)) {
+        W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
+        w2_sched_add(S, lay.c0, CH, CLS);
+        w2_sched_add(S, lay.c2, CLS, CLS);
         hipLaunchKernelGGL(pw2_last_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
-                           packed, msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N,
+                           packed, S, msg3(lay.layer[lay.L - 1]), lay.c0, lay.c2, lay.c4_w, lay.c4_b, opart, ml, nsplit, N,
                            Npad, feat, feat_out, normed, normed_s, conf);
         return hipGetLastError();
     }

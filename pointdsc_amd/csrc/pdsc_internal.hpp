@@ -29,16 +29,28 @@ __host__ __device__ inline size_t mpack_floats(int N) {
 __host__ __device__ inline int mpack_tile(int ti, int tj, int nt) { return ti * nt - ti * (ti - 1) / 2 + (tj - ti); }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Three-plane weight blocks: block (t, ks) = 32 outputs x one 16-input k-step,
+// planes hi / mid / lo of 64 lanes x 8 halfs (1 KiB) each, blocks t-major.
+// Element (o, c) of plane p sits at w3_index(o, c, in) + 512 p (halfs), with
+// lane (h, n), n = o % 32, holding positions 8h .. 8h+7 of the k-step in
+// qk_pos order (bits 2 and 3 of c % 16 swapped).
+constexpr int W3_BLOCK = 3 * 512;  // halfs per block
+__host__ __device__ inline size_t w3_index(int o, int c, int in) {
+    const int t = o >> 5, n = o & 31, ks = c >> 4, q = c & 15;
+    const int pos = (q & ~12) | ((q & 4) << 1) | ((q & 8) >> 1);
+    return ((size_t)t * (in / 16) + ks) * W3_BLOCK + (size_t)(32 * (pos >> 3) + n) * 8 + (pos & 7);
+}
+
 // ---- packed weights --------------------------------------------------------
 // A "dense" layer (Conv1d k=1 [+BN] [+ReLU]) is stored as
 //   W  : OUT*IN floats in MFMA fragment order:
 //        Wpk[((jt*(IN/8) + g)*64 + lane)*4 + e] = W[jt*32 + (lane&31)][(lane>>5)*(IN/2) + 4g + e]
 //   bias[OUT], alpha[OUT], beta[OUT]   (alpha=1, beta=0 when no BN)
-// A dense layer in the packed blob: W as three fp16 planes [out][in] (hi, mid,
-// lo: W * 2^s = hi + mid + lo, s chosen per layer so max|W| 2^s <= 2^14, inputs
-// of each 16-wide k-step in qk_pos order) occupying 1.5*out*in floats at w --
-// or, for PDSC_PRECISION_F32, W itself fp32 [out][in] in the first out*in of
-// them -- then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
+// A dense layer in the packed blob: W as three fp16 planes (hi, mid, lo: W * 2^s
+// = hi + mid + lo, s chosen per layer so max|W| 2^s <= 2^14) in MFMA-fragment
+// blocks (w3_index) occupying 1.5*out*in floats at w -- or, for
+// PDSC_PRECISION_F32, W itself fp32 [out][in] in the first out*in of them --
+// then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
 struct DenseOff {
     size_t w, bias, alpha, beta, scale;
 };
@@ -178,6 +190,13 @@ hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, 
                               hipStream_t s);
 hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
                         hipStream_t s);
+
+// training-mode forward pieces (training.hip)
+// feats: the split normed copy [B][N][2][128] fp16 (H3) or normed [B][N][128] (f32)
+hipError_t launch_feat_sim(const void *feats, bool f32, int B, int N, const float *sigma, float *M, hipStream_t s);
+size_t sm_loss_partial_doubles(int B, int N);
+hipError_t launch_sm_loss(const float *M, const float *labels, int B, int N, int balanced, double *part, float *loss,
+                          hipStream_t s);
 
 // correspondence construction (corr.hip)
 #define HIP_RET(expr)                         \

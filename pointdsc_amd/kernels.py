@@ -255,6 +255,44 @@ def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
     return trans, labels
 
 
+def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=False):
+    """Training-mode forward (models/PointDSC.py:158-163, :176, :182, :189-191) for
+    B pairs: (final_trans [B,4,4], confidence [B,N], M [B,N,N] | None,
+    seeds [B,S] | None).  Forward only: no gradients flow through the HIP path."""
+    corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
+    B, N, _ = src.shape
+    _check_inputs(cfg, corr_pos, src, tgt)
+    dev = src.device
+    L = _lib.load()
+    nb = L.pdsc_forward_training_workspace_bytes(ctypes.byref(cfg), B, N)
+    if nb == 0:
+        raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
+    ws = _workspace(nb, dev)
+    trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
+    conf = torch.empty((B, N), dtype=torch.float32, device=dev)
+    M = torch.empty((B, N, N), dtype=torch.float32, device=dev) if want_M else None
+    seeds = torch.empty((B, int(N * cfg.ratio)), dtype=torch.int32, device=dev) if want_seeds else None
+    check(L.pdsc_forward_training(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
+                                  _p(trans), _p(conf), _p(M), _p(seeds), _p(ws), nb, _stream(dev)),
+          "pdsc_forward_training")
+    return trans, conf, M, seeds
+
+
+def spectral_matching_loss(M, gt_labels, balanced=True):
+    """SpectralMatchingLoss (libs/loss.py:115-139) forward: a device scalar tensor."""
+    M, gt = _dev(M, "M"), _dev(gt_labels, "gt_labels")
+    if M.dim() != 3 or M.shape[1] != M.shape[2] or gt.shape != M.shape[:2]:
+        raise ValueError(f"M {tuple(M.shape)} must be [B,N,N] and gt_labels {tuple(gt.shape)} [B,N]")
+    B, N = gt.shape
+    L = _lib.load()
+    nb = L.pdsc_spectral_matching_loss_workspace_bytes(B, N)
+    ws = _workspace(nb, M.device)
+    loss = torch.empty((), dtype=torch.float32, device=M.device)
+    check(L.pdsc_spectral_matching_loss(_p(M), _p(gt), B, N, int(bool(balanced)), _p(loss), _p(ws), nb,
+                                        _stream(M.device)), "pdsc_spectral_matching_loss")
+    return loss
+
+
 class ForwardPlan:
     """Reusable workspace + outputs for repeated batched forwards of one (B, N).
 

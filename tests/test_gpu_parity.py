@@ -16,8 +16,9 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (ENVELOPE, FEAT_FLOOR, LOGIT_FLOOR, assert_knn_equivalent, assert_rigid, assert_seeds_equivalent,
-                      assert_seeds_near_ties, encoder_fp64, golden_hparams, golden_names, golden_state_dict,
+from conftest import (ENVELOPE, FEAT_FLOOR, LOGIT_FLOOR, assert_knn_equivalent, assert_poses_close, assert_rigid,
+                      assert_seeds_equivalent,
+                      assert_seeds_near_ties, fp32_envelope, golden_hparams, golden_names, golden_state_dict,
                       load_golden, seed_H_rank)
 
 pytestmark = pytest.mark.gpu
@@ -46,22 +47,11 @@ def _inputs(g, dev):
     return (_t(g["corr_pos"][None], dev), _t(g["src_keypts"][None], dev), _t(g["tgt_keypts"][None], dev))
 
 
-def _fp64(name, g, dev):
-    if name not in _FP64:
-        _FP64[name] = encoder_fp64(g, golden_state_dict(g), dev)
-    return _FP64[name]
-
-
 def _envelope(name, g, dev):
-    """(feature error bound x max|f|, logit error bound) vs exact arithmetic, and the yardstick."""
-    f64, c64 = _fp64(name, g, dev)
-    mx = np.abs(f64).max()
-    e_c = np.abs(g["confidence"] - c64).max()
-    if len(g["corr_features"]):
-        e_f = np.abs(g["corr_features"] - f64).max() / mx
-    else:  # N > 5000 goldens keep the logits only
-        e_f = None
-    return e_f, e_c, f64, c64, mx
+    """(fp32 feature noise / max|f|, fp32 logit noise, f64, c64, max|f|): conftest.fp32_envelope, cached."""
+    if name not in _FP64:
+        _FP64[name] = fp32_envelope(g, golden_state_dict(g), dev)
+    return _FP64[name]
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -94,14 +84,11 @@ def test_encoder_and_classifier(name, precision, gpu_device):
     assert ours_c <= ENVELOPE * e_c + LOGIT_FLOOR, (ours_c, e_c)
     f = feat[0].double().cpu().numpy()
     ours_f = np.abs(f - f64).max() / mx
-    if e_f is not None:
-        assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (ours_f, e_f)
-    else:
-        assert ours_f <= 5e-5, ours_f  # no reference features stored (N > 5000): absolute fp32-level bound
+    assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (ours_f, e_f)
+    # normed rows are unit vectors: their error is the feature error relative to the row norm
     n64 = f64 / np.maximum(np.linalg.norm(f64, axis=1, keepdims=True), 1e-12)
-    e_n = (np.abs(g["corr_features"] / np.maximum(np.linalg.norm(g["corr_features"], axis=1, keepdims=True), 1e-12)
-                  - n64).max() if e_f is not None else 5e-5)
-    assert np.abs(normed[0].double().cpu().numpy() - n64).max() <= ENVELOPE * e_n + FEAT_FLOOR
+    rel_row = (np.abs(f - f64).max(1) / np.maximum(np.linalg.norm(f64, axis=1), 1e-12)).max()
+    assert np.abs(normed[0].double().cpu().numpy() - n64).max() <= 2 * rel_row + 1e-6
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -121,9 +108,8 @@ def test_h3_matches_exact_fp32(name, gpu_device):
                   L[0].cpu().numpy())
     e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
     (fh, ch, Th, Lh), (ff, cf, Tf, Lf) = out["h3"], out["f32"]
-    ef = e_f if e_f is not None else 2e-5
-    assert np.abs(fh - ff).max() / mx <= ENVELOPE * ef + FEAT_FLOOR
-    assert np.abs(ch - cf).max() <= ENVELOPE * e_c + LOGIT_FLOOR
+    assert np.abs(fh - ff).max() / mx <= 2 * ENVELOPE * e_f + FEAT_FLOOR  # each within ENVELOPE of exact
+    assert np.abs(ch - cf).max() <= 2 * ENVELOPE * e_c + LOGIT_FLOOR
     assert np.array_equal(Lh, Lf)
     np.testing.assert_allclose(Th, Tf, atol=POSE_ATOL)
 
@@ -171,7 +157,8 @@ def test_nsm_chain(name, precision, gpu_device):
                                                                    float(g["inlier_threshold"]))
     st = seed_trans[0].cpu().numpy()
     ok = seed_H_rank(g) > 1e-5
-    np.testing.assert_allclose(st[ok], g["seed_trans"][ok], atol=POSE_ATOL)
+    kn = g["knn_idx"][ok]
+    assert_poses_close(st[ok], g["seed_trans"][ok], g["src_keypts"][kn], g["tgt_keypts"][kn], w_ref[ok], POSE_ATOL)
     for s in np.nonzero(~ok)[0]:
         assert_rigid(st[s], g["src_keypts"][g["knn_idx"][s]], g["tgt_keypts"][g["knn_idx"][s]], w_ref[s])
     assert np.array_equal(fit[0].cpu().numpy()[ok], g["seed_fitness"][ok])

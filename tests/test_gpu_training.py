@@ -1,0 +1,174 @@
+"""the training branch's evaluation-mode forward (the
+validation loop of libs/trainer.py:202-239: models/PointDSC.py:158-163, :176,
+:182, :189-191) and SpectralMatchingLoss (libs/loss.py:115-139) on the HIP path,
+against the reference's own outputs on B-pair batches (tests/golden/train_*.npz,
+made by tools/gen_goldens.py from the reference's models.PointDSC and
+libs.loss).
+
+Float bar (as tests/test_gpu_parity.py): the distance of the HIP
+M and logits from exact (fp64) arithmetic is at most ENVELOPE x the fp32 noise
+of the case (the reference's own distance, and that of four re-ordered fp32
+evaluations), plus a floor at fp32 resolution.  Seeds (argsort of the logits)
+agree up to near-ties; final_trans within 1e-4 of the reference where the
+chosen hypothesis is the same."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ENVELOPE, LOGIT_FLOOR, assert_seeds_equivalent, encoder_torch, golden_hparams, \
+    golden_state_dict, load_golden
+
+pytestmark = pytest.mark.gpu
+
+TRAIN = ["train_small", "train_rel_1k", "train_kitti_1k"]
+PRECISIONS = ["h3", "f32"]
+M_FLOOR = 2e-6
+_ENV = {}
+
+
+def _t(a, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev).to(dtype)
+
+
+def _model(g, dev, precision):
+    from pointdsc_amd.PointDSC import PointDSC
+    hp = golden_hparams(g)
+    m = PointDSC(in_dim=6, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
+                 nms_radius=hp["nms_radius"], precision=precision)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state_dict(g).items()})
+    return m.to(dev).eval()
+
+
+def _sim64(f, sigma):
+    n = f / np.linalg.norm(f, axis=1, keepdims=True)
+    M = np.clip(1.0 - (1.0 - n @ n.T) / float(np.float32(sigma)) ** 2, 0.0, 1.0)
+    np.fill_diagonal(M, 0.0)
+    return M
+
+
+def _envelope(name, g, dev):
+    """Per pair: (M64 [N,N], c64 [N], fp32 M noise, fp32 logit noise)."""
+    if name in _ENV:
+        return _ENV[name]
+    sd = golden_state_dict(g)
+    sigma = float(np.asarray(sd["sigma"]).reshape(-1)[0])
+    out = []
+    for b in range(g["corr_pos"].shape[0]):
+        gb = {k: g[k] for k in ("sigma_d", "num_layers")}
+        gb.update(corr_pos=g["corr_pos"][b], src_keypts=g["src_keypts"][b], tgt_keypts=g["tgt_keypts"][b])
+        f64, c64 = encoder_torch(gb, sd, dev)
+        M64 = _sim64(f64, sigma)
+        e_m = np.abs(g["M_rows"][b] - M64[:len(g["M_rows"][b])]).max()
+        e_c = np.abs(g["final_labels"][b] - c64).max()
+        for s in range(4):
+            f32, c32 = encoder_torch(gb, sd, dev, torch.float32, seed=s)
+            e_m = max(e_m, np.abs(_sim64(f32, sigma) - M64).max())
+            e_c = max(e_c, np.abs(c32 - c64).max())
+        out.append((M64, c64, e_m, e_c))
+    _ENV[name] = out
+    return out
+
+
+def _fitness(T, src, tgt, tau):
+    r = np.linalg.norm(src @ T[:3, :3].T.astype(np.float64) + T[:3, 3] - tgt, axis=-1)
+    return int((r < tau).sum())
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("name", TRAIN)
+def test_training_forward_vs_reference(name, precision, gpu_device):
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    from pointdsc_amd.loss import SpectralMatchingLoss
+    g = load_golden(name)
+    m = _model(g, gpu_device, precision)
+    corr, src, tgt = (_t(g[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    B, N = g["final_labels"].shape
+    with torch.no_grad():
+        res = m({"corr_pos": corr, "src_keypts": src, "tgt_keypts": tgt})
+    trans, conf, M, seeds = kernels.forward_training(m.pdsc_config(), m.packed_weights(), corr, src, tgt,
+                                                     want_seeds=True)
+    assert res["final_trans"].shape == (B, 4, 4) and res["final_labels"].shape == (B, N)
+    assert res["M"].shape == (B, N, N)
+    assert torch.equal(res["M"], M) and torch.equal(res["final_labels"], conf) and torch.equal(res["final_trans"], trans)
+    M, conf, trans, seeds = (t.cpu().numpy() for t in (M, conf, trans, seeds))
+    env = _envelope(name, g, gpu_device)
+    tau = float(g["inlier_threshold"])
+    for b in range(B):
+        M64, c64, e_m, e_c = env[b]
+        assert np.all(np.diagonal(M[b]) == 0.0) and M[b].min() >= 0.0 and M[b].max() <= 1.0
+        em = np.abs(M[b] - M64).max()
+        assert em <= ENVELOPE * e_m + M_FLOOR, f"pair {b}: M err {em:.3g} vs fp32 noise {e_m:.3g}"
+        ec = np.abs(conf[b] - c64).max()
+        tol_c = ENVELOPE * e_c + LOGIT_FLOOR
+        assert ec <= tol_c, f"pair {b}: logit err {ec:.3g} vs fp32 noise {e_c:.3g}"
+        np.testing.assert_allclose(M[b].astype(np.float64).sum(-1), g["M_row_sums"][b],
+                                   atol=N * (ENVELOPE * e_m + M_FLOOR))
+        assert_seeds_equivalent(seeds[b], g["seeds"][b], g["final_labels"][b].astype(np.float64), tol=2 * tol_c)
+        if np.array_equal(seeds[b], g["seeds"][b]) and np.abs(trans[b] - g["final_trans"][b]).max() > 1e-4:
+            # a different best hypothesis: only a fitness tie with the reference's may explain it
+            s, t = g["src_keypts"][b].astype(np.float64), g["tgt_keypts"][b].astype(np.float64)
+            assert _fitness(trans[b], s, t, tau) == int(g["seed_fitness"][b].max()), f"pair {b}"
+    # the loss: fp64 sums of our M, and against the reference's value through the fp64 yardstick
+    for balanced, key in ((True, "sm_loss_balanced"), (False, "sm_loss_mse")):
+        ours = float(SpectralMatchingLoss(balanced)(res["M"], _t(g["gt_labels"], gpu_device)))
+        np.testing.assert_allclose(ours, O.spectral_matching_loss(M, g["gt_labels"], balanced), rtol=2e-7)
+        l64 = O.spectral_matching_loss(np.stack([e[0] for e in env]), g["gt_labels"], balanced)
+        bound = ENVELOPE * abs(float(g[key]) - l64) + 2e-6 * l64
+        assert abs(ours - l64) <= max(bound, 1e-4 * l64), (ours, float(g[key]), l64)
+
+
+def test_loss_on_reference_M(gpu_device):
+    """SpectralMatchingLoss on the reference's own M (train_small holds it whole)
+    reproduces the reference's loss to fp32 resolution."""
+    from pointdsc_amd.loss import SpectralMatchingLoss
+    g = load_golden("train_small")
+    M, gt = _t(g["M"], gpu_device), _t(g["gt_labels"], gpu_device)
+    np.testing.assert_allclose(float(SpectralMatchingLoss(True)(M, gt)), float(g["sm_loss_balanced"]), rtol=2e-6)
+    np.testing.assert_allclose(float(SpectralMatchingLoss(False)(M, gt)), float(g["sm_loss_mse"]), rtol=2e-6)
+
+
+@pytest.mark.parametrize("B,N,labels", [(1, 1, "ones"), (2, 67, "random"), (3, 130, "zeros"), (2, 200, "ones"),
+                                        (4, 513, "random")])
+def test_loss_edge_cases(B, N, labels, gpu_device):
+    """Ragged N (not a multiple of the 64-row strip), a single point, no positives
+    (relu(sum gt - 1) + 1 = 1) and all positives, against the fp64 restatement."""
+    from oracle import pdsc_oracle as O
+    from pointdsc_amd import kernels
+    rng = np.random.RandomState(B * 1000 + N)
+    M = rng.rand(B, N, N).astype(np.float32)
+    gt = {"ones": np.ones((B, N)), "zeros": np.zeros((B, N)),
+          "random": (rng.rand(B, N) < 0.3)}[labels].astype(np.float32)
+    for balanced in (True, False):
+        ours = float(kernels.spectral_matching_loss(_t(M, gpu_device), _t(gt, gpu_device), balanced))
+        np.testing.assert_allclose(ours, O.spectral_matching_loss(M, gt, balanced), rtol=2e-7)
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_feature_similarity_random(precision, gpu_device):
+    """M on ragged N without the loss outputs (want_M) and the NULL-M path: the
+    M-less call returns the same trans and logits."""
+    from pointdsc_amd import kernels
+    g = load_golden("train_small")
+    m = _model(g, gpu_device, precision)
+    corr, src, tgt = (_t(g[k][:, :203], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    t1, c1, M1, s1 = kernels.forward_training(m.pdsc_config(), m.packed_weights(), corr, src, tgt, want_seeds=True)
+    t2, c2, M2, _ = kernels.forward_training(m.pdsc_config(), m.packed_weights(), corr, src, tgt, want_M=False)
+    assert M2 is None and torch.equal(t1, t2) and torch.equal(c1, c2)
+    _, normed, c0 = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, kernels.compat(
+        src, tgt, m.sigma_spat.detach()), want_features=False)
+    n = normed.double().cpu().numpy()
+    for b in range(2):
+        ref = _sim64(n[b], 1.0)
+        assert np.abs(M1[b].cpu().numpy() - ref).max() <= 5e-6
+        order = np.argsort(-c1[b].double().cpu().numpy(), kind="stable")[:20]
+        assert np.array_equal(s1[b].cpu().numpy(), order)
+
+
+def test_train_mode_raises(gpu_device):
+    g = load_golden("train_small")
+    m = _model(g, gpu_device, "h3").train()
+    corr, src, tgt = (_t(g[k], gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    with pytest.raises(NotImplementedError):
+        m({"corr_pos": corr, "src_keypts": src, "tgt_keypts": tgt})

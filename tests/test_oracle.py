@@ -133,3 +133,30 @@ def test_rigid_transform_recovers_pose():
     T = O.rigid_transform_3d(A, B.astype(np.float32), np.ones((4, 50), np.float32))
     np.testing.assert_allclose(T[:, :3, :3], R, atol=1e-5)
     np.testing.assert_allclose(T[:, :3, 3], t, atol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["train_small", "train_rel_1k", "train_kitti_1k"])
+def test_training_forward_goldens(name):
+    """The oracle's eval-mode training forward and SpectralMatchingLoss
+    (models/PointDSC.py:158-191, libs/loss.py:115-139) against the reference's
+    own outputs: seeds identical, logits / M rows within the fp32 noise of this
+    2-layer network, the loss to fp32 resolution on the reference's M."""
+    g = load_golden(name)
+    sd = golden_state_dict(g)
+    hp = golden_hparams(g)
+    B, N = g["final_labels"].shape
+    Ms = []
+    for b in range(B):
+        o = O.forward_training(g["corr_pos"][b], g["src_keypts"][b], g["tgt_keypts"][b], sd, hp["num_layers"],
+                               inlier_threshold=hp["inlier_threshold"])
+        assert np.array_equal(o["seeds"], g["seeds"][b])
+        np.testing.assert_allclose(o["final_labels"], g["final_labels"][b], atol=1e-4)
+        np.testing.assert_allclose(o["M"][:8], g["M_rows"][b], atol=1e-4)
+        assert np.all(np.diagonal(o["M"]) == 0) and np.array_equal(np.diagonal(o["M"]), g["M_diag"][b])
+        np.testing.assert_allclose(o["final_trans"], g["final_trans"][b], atol=1e-4)
+        Ms.append(o["M"])
+    for balanced, key in ((True, "sm_loss_balanced"), (False, "sm_loss_mse")):
+        np.testing.assert_allclose(O.spectral_matching_loss(np.stack(Ms), g["gt_labels"], balanced), g[key],
+                                   rtol=2e-5)
+        if "M" in g:
+            np.testing.assert_allclose(O.spectral_matching_loss(g["M"], g["gt_labels"], balanced), g[key], rtol=2e-6)

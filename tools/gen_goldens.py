@@ -193,6 +193,61 @@ def run_case(name):
           f"({os.path.getsize(path) / 1e3:.0f} kB)")
 
 
+def run_training(name, L, N, B, preset, pseed, ratio):
+    """The reference's TRAINING-mode forward (no 'testing' key, models/PointDSC.py:158-163,
+    176, 182, 189-191) on B pairs at once, plus SpectralMatchingLoss (libs/loss.py:115-139),
+    balanced and not, against the pairs' ground-truth labels."""
+    import torch
+    sys.path.insert(0, REF)
+    import models.PointDSC as refmod
+    from libs.loss import SpectralMatchingLoss
+    torch.set_num_threads(1)
+    p = PRESETS[preset]
+    pairs = [synthetic_pair(N, pseed * 1000 + b, preset, ratio) for b in range(B)]
+    sd_np = trained_state_dict(preset, L, 10.0, 1.0)  # classifier shift: distinct positive logits
+    model = refmod.PointDSC(in_dim=6, num_layers=L, num_channels=128, num_iterations=10, ratio=0.1,
+                            inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40,
+                            nms_radius=p["nms_radius"])
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+    model.eval()
+    rec = {}
+    o_seed = model.cal_seed_trans
+
+    def seed_wrap(seeds, *a):
+        rec["seeds"] = seeds.clone()
+        out = o_seed(seeds, *a)
+        rec["seed_out"] = [t.clone() for t in out]
+        return out
+
+    model.cal_seed_trans = seed_wrap
+    data = {k: torch.from_numpy(np.stack([q[k] for q in pairs])) for k in ("corr_pos", "src_keypts", "tgt_keypts")}
+    gt = torch.from_numpy(np.stack([q["gt_labels"] for q in pairs]))
+    with torch.no_grad():
+        res = model(data)
+        loss_b = SpectralMatchingLoss(balanced=True)(res["M"], gt).item()
+        loss_u = SpectralMatchingLoss(balanced=False)(res["M"], gt).item()
+    M = res["M"].numpy()
+    out = dict(num_layers=L, preset=preset, pair_seed=pseed, inlier_ratio=ratio, weights_sha256=weights_digest(sd_np),
+               cls_bias_shift=10.0, cls_scale=1.0, sigma_d=p["sigma_d"], inlier_threshold=p["inlier_threshold"],
+               nms_radius=p["nms_radius"],
+               corr_pos=data["corr_pos"].numpy(), src_keypts=data["src_keypts"].numpy(),
+               tgt_keypts=data["tgt_keypts"].numpy(), gt_labels=gt.numpy(),
+               final_trans=res["final_trans"].numpy(), final_labels=res["final_labels"].numpy(),
+               seeds=rec["seeds"].numpy().astype(np.int64), seed_fitness=rec["seed_out"][1].numpy(),
+               M_row_sums=M.astype(np.float64).sum(-1), M_diag=np.diagonal(M, axis1=1, axis2=2).copy(),
+               M_rows=M[:, :8].copy(), sm_loss_balanced=loss_b, sm_loss_mse=loss_u)
+    if N <= 300:
+        out["M"] = M
+    path = os.path.join(REPO, "tests", "golden", f"train_{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"train_{name}: B={B} N={N} L={L} loss balanced {loss_b:.6g} mse {loss_u:.6g} -> "
+          f"{os.path.relpath(path, REPO)} ({os.path.getsize(path) / 1e3:.0f} kB)")
+
+
+TRAIN_CASES = {"small": (2, 256, 2, "3dmatch", 41, 0.3), "rel_1k": (12, 1000, 2, "3dmatch", 42, 0.3),
+               "kitti_1k": (12, 1000, 1, "kitti", 43, 0.2)}
+
+
 def run_kabsch():
     """The reference's rigid_transform_3d (models/common.py:7-45, LAPACK SVD on the
     CPU) on degenerate inputs: all-zero and negative weights (H = 0: LAPACK's
@@ -236,9 +291,11 @@ def run_kabsch():
 
 
 if __name__ == "__main__":
-    names = sys.argv[1:] or list(CASES) + ["kabsch"]
+    names = sys.argv[1:] or list(CASES) + ["kabsch"] + ["train_" + t for t in TRAIN_CASES]
     for n in names:
         if n == "kabsch":
             run_kabsch()
+        elif n.startswith("train_"):
+            run_training(n[6:], *TRAIN_CASES[n[6:]])
         else:
             run_case(n)

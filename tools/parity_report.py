@@ -21,41 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-from conftest import golden_hparams, golden_names, golden_state_dict, load_golden  # noqa: E402
+from conftest import fp32_envelope, golden_hparams, golden_names, golden_state_dict, load_golden  # noqa: E402
 
 
 def _t(x, dev, dtype=torch.float32):
     return torch.from_numpy(np.ascontiguousarray(x)).to(dev, dtype)
-
-
-def encoder64(g, sd, dev):
-    """Exact-arithmetic (torch fp64) restatement of models/PointDSC.py:65-77, :156, :171
-    on the bit-exact fp32 M: the yardstick both fp32 implementations are measured against."""
-    from pointdsc_amd import kernels
-    W = {k: torch.as_tensor(np.asarray(v)).to(dev).double() for k, v in sd.items() if np.asarray(v).dtype != np.int64}
-
-    def conv(x, n):
-        return x @ W[n + ".weight"][:, :, 0].T + W[n + ".bias"]
-
-    def bn(x, n):
-        a = W[n + ".weight"] / torch.sqrt(W[n + ".running_var"] + 1e-5)
-        return x * a + (W[n + ".bias"] - W[n + ".running_mean"] * a)
-
-    src, tgt = (_t(g[k][None], dev) for k in ("src_keypts", "tgt_keypts"))
-    M = kernels.compat(src, tgt, torch.tensor([float(np.float32(g["sigma_d"]))], device=dev))[0].double()
-    f = conv(_t(g["corr_pos"], dev).double(), "encoder.layer0")
-    for i in range(int(g["num_layers"])):
-        p = f"encoder.blocks.PointCN_layer_{i}"
-        f = torch.relu(bn(conv(f, p + ".0"), p + ".1"))
-        p = f"encoder.blocks.NonLocal_layer_{i}"
-        q, k, v = (conv(f, f"{p}.projection_{c}") for c in "qkv")
-        A = torch.softmax(M * (q @ k.T) / 128 ** 0.5, -1)
-        h = torch.relu(bn(conv(A @ v, p + ".fc_message.0"), p + ".fc_message.1"))
-        h = torch.relu(bn(conv(h, p + ".fc_message.3"), p + ".fc_message.4"))
-        f = f + conv(h, p + ".fc_message.6")
-    h = torch.relu(conv(f, "classification.0"))
-    h = torch.relu(conv(h, "classification.2"))
-    return f.cpu().numpy(), conv(h, "classification.4")[:, 0].cpu().numpy()
 
 
 def report(name, precision, dev):
@@ -65,27 +35,29 @@ def report(name, precision, dev):
     hp = golden_hparams(g)
     m = PointDSC(in_dim=6, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
                  inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
-                 nms_radius=hp["nms_radius"], **({} if precision == "h3" else {"precision": precision}))
+                 nms_radius=hp["nms_radius"], precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state_dict(g).items()})
     m = m.to(dev).eval()
     corr, src, tgt = (_t(g[k][None], dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
     cfg, packed = m.pdsc_config(), m.packed_weights()
     M = kernels.compat(src, tgt, m.sigma_spat)
     feat, normed, conf = kernels.encoder(cfg, packed, corr, M)
-    f_ref = g["corr_features"].astype(np.float64)
+    e_f, e_c, f64, c64, _ = fp32_envelope(g, golden_state_dict(g), dev)
+    has_f = len(g["corr_features"]) > 0
+    f_ref = g["corr_features"].astype(np.float64) if has_f else f64
     f = feat[0].double().cpu().numpy()
     n_ref = f_ref / np.maximum(np.linalg.norm(f_ref, axis=1, keepdims=True), 1e-12)
-    out = {"name": name, "precision": precision, "N": int(len(f_ref)),
-           "feat_rel": float(np.abs(f - f_ref).max() / np.abs(f_ref).max()),
+    out = {"name": name, "precision": precision, "N": int(len(f)),
+           "feat_rel": float(np.abs(f - f_ref).max() / np.abs(f_ref).max()) if has_f else None,
            "logit_abs": float(np.abs(conf[0].double().cpu().numpy() - g["confidence"]).max()),
            "logit_range": [float(g["confidence"].min()), float(g["confidence"].max())],
-           "normed_abs": float(np.abs(normed[0].double().cpu().numpy() - n_ref).max())}
-    f64, c64 = encoder64(g, golden_state_dict(g), dev)
+           "normed_abs": float(np.abs(normed[0].double().cpu().numpy() - n_ref).max()) if has_f else None}
     mx = np.abs(f64).max()
-    out["ref_vs_fp64_feat"] = float(np.abs(f_ref - f64).max() / mx)
+    out["ref_vs_fp64_feat"] = float(np.abs(f_ref - f64).max() / mx) if has_f else None
     out["ours_vs_fp64_feat"] = float(np.abs(f - f64).max() / mx)
     out["ref_vs_fp64_logit"] = float(np.abs(g["confidence"] - c64).max())
     out["ours_vs_fp64_logit"] = float(np.abs(conf[0].double().cpu().numpy() - c64).max())
+    out["fp32_noise_feat"], out["fp32_noise_logit"] = float(e_f), float(e_c)
     from oracle import pdsc_oracle as O
     lm_o = O.local_max(g["src_keypts"], conf[0].cpu().numpy(), float(g["nms_radius"]))
     out["lm_mismatch"] = int((lm_o != g["is_local_max"]).sum())
@@ -99,15 +71,17 @@ def report(name, precision, dev):
     out["seed_min_gap_ref"] = float(g["seed_score_min_gap"])
     out["trans_abs"] = float(np.abs(trans[0].cpu().numpy() - g["final_trans"]).max())
     out["label_mismatch"] = int((labels[0].cpu().numpy() != g["final_labels"]).sum())
+    if not has_f:
+        return out
     # stage-isolated NSM chain on the reference's own normed / seeds
     normed_ref = _t(n_ref.astype(np.float32), dev)[None]
     sd = golden_state_dict(g)
     k = g["knn_idx"].shape[1]
-    knn = kernels.seed_knn(normed_ref, _t(g["seeds"][None], dev, torch.int32), k)[0].cpu().numpy()
+    knn = kernels.seed_knn(normed_ref, _t(g["seeds"][None], dev, torch.int32), k, precision=precision)[0].cpu().numpy()
     out["knn_rows_diff"] = int(sum(set(a.tolist()) != set(b.tolist()) for a, b in zip(knn, g["knn_idx"])))
     out["knn_order_diff"] = int((knn != g["knn_idx"]).any(1).sum())
     w, _ = kernels.nsm_weights(normed_ref, src, tgt, _t(g["knn_idx"][None], dev, torch.int32), 10,
-                               _t(sd["sigma"], dev), _t(sd["sigma_spat"], dev))
+                               _t(sd["sigma"], dev), _t(sd["sigma_spat"], dev), precision=precision)
     v = g["leading_eig"]
     out["nsm_w_abs"] = float(np.abs(w[0].cpu().numpy() - v / (v.sum(-1, keepdims=True) + 1e-6)).max())
     return out
