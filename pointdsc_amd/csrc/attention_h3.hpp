@@ -86,7 +86,13 @@ PDSC_DEV size_t vs_off(int key, int half, int c) {
            8 * ((kp >> 3) ^ ((rho >> 2) & 3)) + (kp & 7);
 }
 
+// x = hi + lo (fp16 pair).  The empty asm pins x as the rounded fp32 value:
+// without it the compiler folds a producing multiply into the hi conversion
+// (v_fma_mixlo_f16: one rounding of the exact product) while lo is formed from the
+// fp32-rounded product, so where that product rounds onto an fp16 tie, hi and
+// lo disagree by one fp16 ulp (measured: 1 channel in ~10^4, 1e-4 errors).
 PDSC_DEV void split_h(float x, _Float16 &hi, _Float16 &lo) {
+    asm("" : "+v"(x));
     hi = (_Float16)x;
     lo = (_Float16)(x - (float)hi);
 }

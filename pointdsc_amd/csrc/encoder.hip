@@ -77,7 +77,8 @@ __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__re
     } else if (i < total) {
         _Float16 *wd = reinterpret_cast<_Float16 *>(dw);
         const int o = i / in, c = i % in;
-        const float x = w[i] * sc[1];  // exact (power of two)
+        float x = w[i] * sc[1];  // exact (power of two)
+        asm("" : "+v"(x));       // one hi for both uses (see split_h)
         const _Float16 hi = (_Float16)x;
         const float r1 = x - (float)hi;  // exact
         const _Float16 mid = (_Float16)r1;
@@ -745,6 +746,9 @@ constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
 constexpr size_t PW2_LDS = 2 * PW2_SLOT + PW2_COEF * sizeof(float);
 constexpr int W2_MAXCH = 24;
+#ifndef PW2_MID_OCC
+#define PW2_MID_OCC 2
+#endif
 
 struct W2Sched {                 // chunk c: np[c] pieces of 1 KiB starting at pk-halfs off[c]
     uint32_t off[W2_MAXCH];
@@ -1106,7 +1110,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *_
 }
 
 // combine_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1}.
-__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
+__global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
                                                                PwDense4 d, const float *__restrict__ opart,
                                                                const float *__restrict__ ml, int nsplit, int N,
                                                                int Npad, float *__restrict__ featL,

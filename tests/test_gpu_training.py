@@ -160,7 +160,7 @@ def test_feature_similarity_random(precision, gpu_device):
         src, tgt, m.sigma_spat.detach()), want_features=False)
     n = normed.double().cpu().numpy()
     for b in range(2):
-        ref = _sim64(n[b], 1.0)
+        ref = _sim64(n[b], float(m.sigma.detach().cpu()))
         assert np.abs(M1[b].cpu().numpy() - ref).max() <= 5e-6
         order = np.argsort(-c1[b].double().cpu().numpy(), kind="stable")[:20]
         assert np.array_equal(s1[b].cpu().numpy(), order)
