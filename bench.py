@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--f32-steps", type=int, default=3, help="steps of the exact-fp32 leg (0 = skip)")
     ap.add_argument("--path-n", type=int, default=5000, help="N of the compat+NSM path roofline (0 = skip)")
     ap.add_argument("--path-pairs", type=int, default=8)
     ap.add_argument("--launcher-selftest", action="store_true",
@@ -450,6 +451,29 @@ def main():
                   "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1)}
         del plan1
 
+        # ---- the exact-fp32 mode (pdsc_config.precision = f32: fp32 MFMA 32x32x2 contractions)
+        # on the same resident batch: its rate, and its agreement with the headline (3xf16) path
+        exact = None
+        if args.f32_steps > 0:
+            model.precision = "f32"
+            cfg32, packed32 = model.pdsc_config(), model.packed_weights()
+            plan32 = kernels.ForwardPlan(cfg32, packed32, P, N, dev)
+            plan32.run(corr, src, tgt)
+            plan.run(corr, src, tgt)
+            torch.cuda.synchronize(dev)
+            t_lab, t_tr = plan.labels.clone(), plan.trans.clone()
+            t0 = time.perf_counter()
+            for _ in range(args.f32_steps):
+                plan32.run(corr, src, tgt)
+            torch.cuda.synchronize(dev)
+            e32 = (time.perf_counter() - t0) / args.f32_steps
+            exact = {"precision": "f32 (exact-fp32 MFMA contractions)", "ms_per_step": round(e32 * 1e3, 3),
+                     "value": round(P * N / e32, 1), "steps": args.f32_steps,
+                     "labels_equal_frac": float((plan32.labels == t_lab).float().mean()),
+                     "max_pose_diff_vs_h3": float((plan32.trans - t_tr).abs().max())}
+            model.precision = "h3"
+            del plan32, packed32
+
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             from oracle import pdsc_oracle as O
@@ -475,7 +499,7 @@ def main():
             "metric": "correspondence-pairs/sec through NSM (N=1k/5k) at 1/2/4/8 GPUs; 3DMatch recall parity",
             "value": round(value, 1), "unit": "correspondences/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 (3xf16-split contractions)",
             "dtype_note": "fp32 inputs, outputs and accumulation; the attention, 1x1-conv and kNN/NSM "
                           "contractions run as 3 fp16 MFMA products (hi*hi + hi*lo + lo*hi) per fp32 product",
             "data": "synthetic",
@@ -488,7 +512,7 @@ def main():
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
-            "stages_ms": stages, "single_pair": single, "cpu_baseline": cpu,
+            "stages_ms": stages, "single_pair": single, "exact_f32": exact, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

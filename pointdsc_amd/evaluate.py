@@ -85,6 +85,51 @@ def aggregate(stats, n_scenes=None):
     return out
 
 
+def report_lines(stats, n_scenes=None):
+    """The summary lines evaluation/test_3DMatch.py:141-176 logs, from [P, 12] rows:
+    per scene, the mean over scenes and the all-pair means (same wording and
+    rounding, so the logs of the two builds diff line by line)."""
+    stats = np.asarray(stats, dtype=np.float64)
+    scenes = sorted(set(stats[:, 11].astype(int).tolist())) if n_scenes is None else list(range(n_scenes))
+    lines, vals = [], []
+    for i, s in enumerate(scenes):
+        st = stats[stats[:, 11].astype(int) == s]
+        if len(st) == 0:
+            continue
+        v = st.mean(0)
+        v[1], v[2] = _mean_success_only(st, 1), _mean_success_only(st, 2)
+        vals.append(v)
+        lines.append(f"Scene {i}th: Reg Recall={v[0] * 100:.2f}%  Mean RE={v[1]:.2f}  Mean TE={v[2]:.2f}  "
+                     f"Mean Precision={v[6] * 100:.2f}%  Mean Recall={v[7] * 100:.2f}%  Mean F1={v[8] * 100:.2f}%")
+    if vals:
+        a = np.stack(vals).mean(0)
+        lines += [f"All {len(vals)} scenes, Mean Reg Recall={a[0] * 100:.2f}%, Mean Re={a[1]:.2f}, Mean Te={a[2]:.2f}",
+                  f"\tInput:  Mean Inlier Num={a[3]:.2f}(ratio={a[4] * 100:.2f}%)",
+                  f"\tOutput: Mean Inlier Num={a[5]:.2f}(precision={a[6] * 100:.2f}%, recall={a[7] * 100:.2f}%, "
+                  f"f1={a[8] * 100:.2f}%)",
+                  f"\tMean model time: {a[9]:.2f}s, Mean data time: {a[10]:.2f}s"]
+    p = stats.mean(0)
+    ok = stats[:, 0] == 1
+    c = stats[ok].mean(0) if ok.any() else np.full(stats.shape[1], np.nan)
+    lines += ["*" * 40,
+              f"All {stats.shape[0]} pairs, Mean Reg Recall={p[0] * 100:.2f}%, Mean Re={c[1]:.2f}, Mean Te={c[2]:.2f}",
+              f"\tInput:  Mean Inlier Num={p[3]:.2f}(ratio={p[4] * 100:.2f}%)",
+              f"\tOutput: Mean Inlier Num={p[5]:.2f}(precision={p[6] * 100:.2f}%, recall={p[7] * 100:.2f}%, "
+              f"f1={p[8] * 100:.2f}%)",
+              f"\tMean model time: {p[9]:.2f}s, Mean data time: {p[10]:.2f}s"]
+    return lines
+
+
+def save_outputs(stats, log_path=None, npy_path=None, n_scenes=None):
+    """The driver's outputs (test_3DMatch.py:238-241): the summary log and, with
+    --save_npy, the [P, 12] float64 stats matrix (np.save, no pickle)."""
+    if log_path:
+        with open(log_path, "w") as f:
+            f.write("\n".join(report_lines(stats, n_scenes)) + "\n")
+    if npy_path:
+        np.save(npy_path, np.asarray(stats, dtype=np.float64), allow_pickle=False)
+
+
 def evaluate_synthetic(model, n_pairs, num_corr, preset="3dmatch", batch=16, seed=0, device=None,
                        inlier_ratio=0.3):
     """Sharded evaluation over n_pairs synthetic pairs: rank r evaluates pairs
@@ -135,6 +180,8 @@ def main():
     ap.add_argument("--preset", default="3dmatch", choices=list(PRESETS))
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--inlier-ratio", type=float, default=0.3)
+    ap.add_argument("--log", default=None, help="write the test_3DMatch.py-style summary log here")
+    ap.add_argument("--save-npy", default=None, help="np.save the [P, 12] per-pair stats here")
     a = ap.parse_args()
     W = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -150,6 +197,7 @@ def main():
     stats, summary = evaluate_synthetic(m, a.pairs, a.num_corr, a.preset, a.batch, device=dev,
                                         inlier_ratio=a.inlier_ratio)
     if not tdist.is_initialized() or tdist.get_rank() == 0:
+        save_outputs(stats, a.log, a.save_npy)
         print(json.dumps(summary))
     if W > 1:
         tdist.destroy_process_group()

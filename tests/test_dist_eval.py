@@ -136,6 +136,28 @@ def test_aggregate_scene_then_mean():
     assert abs(out["scene_mean"]["te_cm"] - 40.0) < 1e-12
 
 
+def test_report_lines_and_npy(tmp_path):
+    """The driver's outputs (evaluation/test_3DMatch.py:141-176, :238-241): the
+    scene / all-scene / all-pair lines with the reference's wording and numbers,
+    and the [P, 12] float64 stats saved without pickle."""
+    rows = np.zeros((5, 12))
+    rows[:, 0] = [1, 0, 1, 1, 1]
+    rows[:, 1] = [1.0, 99, 3.0, 5.0, 7.0]
+    rows[:, 2] = [10, 999, 30, 50, 70]
+    rows[:, 6:9] = 0.5
+    rows[:, 11] = [0, 0, 0, 1, 1]
+    lines = ev.report_lines(rows)
+    assert lines[0] == ("Scene 0th: Reg Recall=66.67%  Mean RE=2.00  Mean TE=20.00  Mean Precision=50.00%  "
+                        "Mean Recall=50.00%  Mean F1=50.00%")
+    assert lines[1].startswith("Scene 1th: Reg Recall=100.00%  Mean RE=6.00  Mean TE=60.00")
+    assert lines[2] == "All 2 scenes, Mean Reg Recall=83.33%, Mean Re=4.00, Mean Te=40.00"
+    assert "All 5 pairs, Mean Reg Recall=80.00%, Mean Re=4.00, Mean Te=40.00" in lines
+    ev.save_outputs(rows, str(tmp_path / "r.log"), str(tmp_path / "r.npy"))
+    assert (tmp_path / "r.log").read_text().splitlines() == lines
+    back = np.load(tmp_path / "r.npy", allow_pickle=False)
+    assert back.dtype == np.float64 and np.array_equal(back, rows)
+
+
 @pytest.mark.gpu
 def test_evaluate_synthetic_on_device(gpu_device):
     """f2 end to end on one GPU: sharded (world 1) synthetic evaluation through
