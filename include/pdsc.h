@@ -275,6 +275,44 @@ int32_t pdsc_build_correspondences(const float *src_desc, const float *tgt_desc,
                                    int32_t *count, float *corr_pos, float *src_keypts, float *tgt_keypts,
                                    float *labels, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
 
+/* ------------------------------------------- f4 descriptor stage ----------
+ * The open3d calls of demo_registration.py:37-44 / misc/cal_fpfh.py:7-36 on the
+ * GPU (open3d's published algorithms restated; parity with open3d itself is
+ * unpinned).  Points are fp32 [n,3] device arrays; 1 <= n <= 2^31-1.  These
+ * entry points synchronise `stream` before returning (they report grid-range
+ * and capacity errors found on the device).
+ *
+ * pdsc_ply_read_xyz (HOST memory, o3d.io.read_point_cloud): the vertex x, y, z
+ * of a binary_little_endian or ascii PLY.  xyz == NULL: only *n_points.     */
+int32_t pdsc_ply_read_xyz(const char *path, float *xyz, int64_t capacity, int64_t *n_points);
+/* KDTreeSearchParamHybrid(radius, max_nn) for every point of the cloud: nbr
+ * [n,max_nn] (ascending (d^2, index), the point itself first, -1 padded),
+ * dist2 [n,max_nn] fp64 (may be NULL), count [n].  1 <= max_nn <= 128.      */
+size_t pdsc_radius_knn_workspace_bytes(int32_t n);
+int32_t pdsc_radius_knn(const float *pts, int32_t n, float radius, int32_t max_nn, int32_t *nbr, double *dist2,
+                        int32_t *count, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
+/* EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) (utils/pointcloud.py:
+ * 20-21): smallest-eigenvalue eigenvector of the neighbourhood covariance,
+ * (0,0,1) under 3 neighbours; oriented towards viewpoint (device float[3]) or,
+ * when NULL, the cloud's centroid.                                          */
+size_t pdsc_estimate_normals_workspace_bytes(int32_t n, int32_t max_nn);
+int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, const float *viewpoint,
+                              float *normals, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
+/* VoxelDownSample(voxel_size): per-voxel means (normals averaged, then
+ * normalised; normals / out_normals may be NULL), voxels in ascending key
+ * order; out_pts [n,3] capacity; *out_count (device int32) = voxels.         */
+size_t pdsc_voxel_down_sample_workspace_bytes(int32_t n);
+int32_t pdsc_voxel_down_sample(const float *pts, const float *normals, int32_t n, float voxel_size, float *out_pts,
+                               float *out_normals, int32_t *out_count, void *workspace, size_t workspace_bytes,
+                               pdsc_stream_t stream);
+/* compute_fpfh_feature(KDTreeSearchParamHybrid(radius, max_nn)): fpfh [n,33]
+ * fp64 (open3d's feature.data.T); fpfh_normalized [n,33] fp32 = f / (||f|| +
+ * 1e-6) (demo_registration.py:42, may be NULL).  normals must be unit.      */
+size_t pdsc_compute_fpfh_workspace_bytes(int32_t n, int32_t max_nn);
+int32_t pdsc_compute_fpfh(const float *pts, const float *normals, int32_t n, float radius, int32_t max_nn,
+                          double *fpfh, float *fpfh_normalized, void *workspace, size_t workspace_bytes,
+                          pdsc_stream_t stream);
+
 /* ----------------------------------------------- full testing forward ------
  * PointDSC.forward(data) with 'testing' in data (models/PointDSC.py:128-197)
  * for B independent pairs: compat -> encoder -> classifier -> seeds -> kNN ->

@@ -88,6 +88,15 @@ _PROTOS = {
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
                                        c_size_t, vp]),
+    "pdsc_ply_read_xyz": (c_int32, [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
+    "pdsc_radius_knn_workspace_bytes": (c_size_t, [c_int32]),
+    "pdsc_radius_knn": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_estimate_normals_workspace_bytes": (c_size_t, [c_int32, c_int32]),
+    "pdsc_estimate_normals": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, c_size_t, vp]),
+    "pdsc_voxel_down_sample_workspace_bytes": (c_size_t, [c_int32]),
+    "pdsc_voxel_down_sample": (c_int32, [vp, vp, c_int32, c_float, vp, vp, vp, vp, c_size_t, vp]),
+    "pdsc_compute_fpfh_workspace_bytes": (c_size_t, [c_int32, c_int32]),
+    "pdsc_compute_fpfh": (c_int32, [vp, vp, c_int32, c_float, c_int32, vp, vp, vp, c_size_t, vp]),
     "pdsc_forward_training_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_training": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_spectral_matching_loss_workspace_bytes": (c_size_t, [c_int32, c_int32]),

@@ -666,6 +666,110 @@ int32_t pdsc_spectral_matching_loss(const float *M, const float *gt_labels, int3
     return PDSC_OK;
 }
 
+// ------------------------------------------------------ f4 descriptor stage
+int32_t pdsc_ply_read_xyz(const char *path, float *xyz, int64_t capacity, int64_t *n_points) {
+    if (!path || !n_points) return fail(PDSC_ERR_ARG, "null pointer");
+    std::string err;
+    if (ply_read_xyz(path, xyz, capacity, n_points, err) != 0) return fail(PDSC_ERR_ARG, "PLY: %s", err.c_str());
+    return PDSC_OK;
+}
+
+static int check_cloud(const float *pts, int32_t n, float r, int32_t max_nn) {
+    if (!pts) return fail(PDSC_ERR_ARG, "null points");
+    if (n < 1) return fail(PDSC_ERR_ARG, "n=%d", n);
+    if (!(r > 0.0f) || !std::isfinite(r)) return fail(PDSC_ERR_ARG, "radius / voxel size %g must be > 0", (double)r);
+    if (max_nn < 1 || max_nn > 128) return fail(PDSC_ERR_UNSUPPORTED, "max_nn=%d not in [1, 128]", max_nn);
+    return PDSC_OK;
+}
+
+// the device error flags of a grid pass, after the stream drained
+static int grid_status(const GridBufs &G, hipStream_t s) {
+    int e[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(e, G.err, sizeof e, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (e[0]) return fail(PDSC_ERR_ARG, "cloud extent / cell size >= 2^21 cells per axis");
+    if (e[1]) return fail(PDSC_ERR_UNSUPPORTED, "a radius neighbourhood holds > 1024 points within one d^2 bin");
+    return PDSC_OK;
+}
+
+size_t pdsc_radius_knn_workspace_bytes(int32_t n) { return n < 1 ? 0 : grid_workspace_bytes(n); }
+
+int32_t pdsc_radius_knn(const float *pts, int32_t n, float radius, int32_t max_nn, int32_t *nbr, double *dist2,
+                        int32_t *count, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cloud(pts, n, radius, max_nn));
+    if (!nbr || !count || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_radius_knn_workspace_bytes(n)));
+    hipStream_t s = S_(stream);
+    GridBufs G;
+    HIPCHK(build_grid(pts, n, radius, 0.0, ws, G, s));
+    HIPCHK(launch_radius_knn(pts, n, G, radius, max_nn, nbr, dist2, count, s));
+    return grid_status(G, s);
+}
+
+size_t pdsc_estimate_normals_workspace_bytes(int32_t n, int32_t max_nn) {
+    if (n < 1 || max_nn < 1) return 0;
+    return grid_workspace_bytes(n) + align_bytes((size_t)n * max_nn * sizeof(int)) + align_bytes((size_t)n * sizeof(int));
+}
+
+int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, const float *viewpoint,
+                              float *normals, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cloud(pts, n, radius, max_nn));
+    if (!normals || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_estimate_normals_workspace_bytes(n, max_nn)));
+    hipStream_t s = S_(stream);
+    char *w = static_cast<char *>(ws);
+    int *nbr = reinterpret_cast<int *>(w + grid_workspace_bytes(n));
+    int *cnt = reinterpret_cast<int *>(reinterpret_cast<char *>(nbr) + align_bytes((size_t)n * max_nn * sizeof(int)));
+    GridBufs G;
+    HIPCHK(build_grid(pts, n, radius, 0.0, ws, G, s));
+    HIPCHK(launch_radius_knn(pts, n, G, radius, max_nn, nbr, nullptr, cnt, s));
+    HIPCHK(launch_normals(pts, n, nbr, cnt, max_nn, G, viewpoint, normals, s));
+    return grid_status(G, s);
+}
+
+size_t pdsc_voxel_down_sample_workspace_bytes(int32_t n) { return n < 1 ? 0 : grid_workspace_bytes(n); }
+
+int32_t pdsc_voxel_down_sample(const float *pts, const float *normals, int32_t n, float voxel_size, float *out_pts,
+                               float *out_normals, int32_t *out_count, void *ws, size_t ws_bytes,
+                               pdsc_stream_t stream) {
+    RET_IF(check_cloud(pts, n, voxel_size, 1));
+    if (!out_pts || !out_count || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_voxel_down_sample_workspace_bytes(n)));
+    hipStream_t s = S_(stream);
+    GridBufs G;
+    HIPCHK(build_grid(pts, n, voxel_size, 0.5 * (double)voxel_size, ws, G, s));
+    HIPCHK(launch_voxel_reduce(pts, normals, n, G, out_pts, out_normals, out_count, s));
+    return grid_status(G, s);
+}
+
+size_t pdsc_compute_fpfh_workspace_bytes(int32_t n, int32_t max_nn) {
+    if (n < 1 || max_nn < 1) return 0;
+    return grid_workspace_bytes(n) + align_bytes((size_t)n * max_nn * sizeof(int)) +
+           align_bytes((size_t)n * max_nn * sizeof(double)) + align_bytes((size_t)n * sizeof(int)) +
+           align_bytes((size_t)n * 33 * sizeof(double));
+}
+
+int32_t pdsc_compute_fpfh(const float *pts, const float *normals, int32_t n, float radius, int32_t max_nn,
+                          double *fpfh, float *fpfh_normalized, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+    RET_IF(check_cloud(pts, n, radius, max_nn));
+    if (!normals || !fpfh || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    RET_IF(need_ws(ws_bytes, pdsc_compute_fpfh_workspace_bytes(n, max_nn)));
+    hipStream_t s = S_(stream);
+    char *w = static_cast<char *>(ws) + grid_workspace_bytes(n);
+    int *nbr = reinterpret_cast<int *>(w);
+    w += align_bytes((size_t)n * max_nn * sizeof(int));
+    double *d2 = reinterpret_cast<double *>(w);
+    w += align_bytes((size_t)n * max_nn * sizeof(double));
+    int *cnt = reinterpret_cast<int *>(w);
+    w += align_bytes((size_t)n * sizeof(int));
+    double *spfh = reinterpret_cast<double *>(w);
+    GridBufs G;
+    HIPCHK(build_grid(pts, n, radius, 0.0, ws, G, s));
+    HIPCHK(launch_radius_knn(pts, n, G, radius, max_nn, nbr, d2, cnt, s));
+    HIPCHK(launch_fpfh(pts, normals, n, nbr, cnt, d2, max_nn, spfh, fpfh, fpfh_normalized, s));
+    return grid_status(G, s);
+}
+
 // ------------------------------------------------- f1 correspondence construction
 size_t pdsc_mutual_nn_workspace_bytes(int32_t Ns, int32_t Nt) {
     return align_bytes((size_t)Ns * 8) + align_bytes((size_t)Nt * 8);

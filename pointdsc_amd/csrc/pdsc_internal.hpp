@@ -1,6 +1,7 @@
 // pdsc_internal.hpp -- launchers and packed-weight layout shared by the
 // translation units of libpdsc (not part of the C ABI).
 #pragma once
+#include <string>
 #include "pdsc_common.hpp"
 #include "../../include/pdsc.h"
 
@@ -197,6 +198,32 @@ hipError_t launch_feat_sim(const void *feats, bool f32, int B, int N, const floa
 size_t sm_loss_partial_doubles(int B, int N);
 hipError_t launch_sm_loss(const float *M, const float *labels, int B, int N, int balanced, double *part, float *loss,
                           hipStream_t s);
+
+// descriptor stage (descriptors.hip)
+struct CloudStats {
+    float mn[3], mx[3];
+    double centroid[3];
+};
+struct GridView {  // points sorted by cell key and the occupied cells
+    unsigned long long *skey, *ukey;
+    int *sidx, *ustart, *ucount, *nruns;
+};
+struct GridBufs {
+    CloudStats *st;
+    GridView view;
+    int *err;  // [0] extent / cell >= 2^21, [1] a kNN candidate set over capacity
+};
+size_t grid_workspace_bytes(int n);
+hipError_t build_grid(const float *pts, int n, double cell, double half, void *ws, GridBufs &G, hipStream_t s);
+hipError_t launch_radius_knn(const float *pts, int n, const GridBufs &G, double radius, int K, int *nbr, double *d2,
+                             int *cnt, hipStream_t s);
+hipError_t launch_normals(const float *pts, int n, const int *nbr, const int *cnt, int K, const GridBufs &G,
+                          const float *viewpoint, float *nrm, hipStream_t s);
+hipError_t launch_voxel_reduce(const float *pts, const float *nrm, int n, const GridBufs &G, float *opts, float *onrm,
+                               int *count, hipStream_t s);
+hipError_t launch_fpfh(const float *pts, const float *nrm, int n, const int *nbr, const int *cnt, const double *d2,
+                       int K, double *spfh, double *out, float *outn, hipStream_t s);
+int ply_read_xyz(const char *path, float *xyz, int64_t capacity, int64_t *n_out, std::string &err);
 
 // correspondence construction (corr.hip)
 #define HIP_RET(expr)                         \
