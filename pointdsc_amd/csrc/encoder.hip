@@ -286,16 +286,8 @@ PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int
 // hi / lo fp16 fragments.
 PDSC_DEV void split8(const float *x, int h, f16x8 &hi, f16x8 &lo) {
     const f32x4 a = *reinterpret_cast<const f32x4 *>(x + 4 * h), b = *reinterpret_cast<const f32x4 *>(x + 8 + 4 * h);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        _Float16 p, q;
-        split_h(a[e], p, q);
-        hi[e] = p;
-        lo[e] = q;
-        split_h(b[e], p, q);
-        hi[4 + e] = p;
-        lo[4 + e] = q;
-    }
+    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    split8x(v, hi, lo);
 }
 
 // One 32-output tile of Y = epi(X W^T + b) for NRT row tiles.  H3: the fp16
@@ -820,8 +812,8 @@ PDSC_DEV void w2_mma(const char *slot, const f16x8 *xh, const f16x8 *xl, f32x16 
         if (j + 2 < NB) w2_frag(bp + (j + 2) * PW2_BLKB, w[(j + 2) % 3]);
         const int t = j / NKS, ks = j % NKS;
         const f16x8(&f)[3] = w[j % 3];
-        acc[t0 + t] = TRANS ? mfma_w3x(f[0], f[1], f[2], xh[ks], xl[ks], acc[t0 + t])
-                            : mfma_xw3(xh[ks], xl[ks], f[0], f[1], f[2], acc[t0 + t]);
+        const f32x16 c = ks == 0 ? zero16() : acc[t0 + t];  // k-step 0 starts from the inline-constant 0
+        acc[t0 + t] = TRANS ? mfma_w3x(f[0], f[1], f[2], xh[ks], xl[ks], c) : mfma_xw3(xh[ks], xl[ks], f[0], f[1], f[2], c);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -834,8 +826,6 @@ PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const W2Sched &S, const f16x8
                        f32x16 (&acc)[OUT / 32], bool active, int wave, int lane) {
     constexpr int NKS = IN / 16, NT = w2_nt(IN, OUT), NCH = OUT / 32 / NT;
     static_assert(NCH * NT == OUT / 32, "chunk tiling");
-#pragma unroll
-    for (int t = 0; t < OUT / 32; ++t) acc[t] = zero16();
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (active) w2_mma<NKS, NT, TRANS>(P.slot(P.c), xh, xl, acc, c * NT, lane);
@@ -856,15 +846,7 @@ PDSC_DEV void w2_coef(float *dst, const float *__restrict__ pk, const DenseOff &
 }
 
 // fp32 -> fp16 hi / lo of 8 values
-PDSC_DEV void split8v(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        _Float16 a, b;
-        split_h(v[e], a, b);
-        hi[e] = a;
-        lo[e] = b;
-    }
-}
+PDSC_DEV void split8v(const float (&v)[8], f16x8 &hi, f16x8 &lo) { split8x(v, hi, lo); }
 
 // Channel of register 8u + e of output tile t for lane half h (transposed layout).
 PDSC_DEV int w2_chan(int t, int u, int e, int h) { return 32 * t + 16 * u + 8 * (e >> 2) + 4 * h + (e & 3); }
