@@ -56,24 +56,6 @@ constexpr int H3_KTB = H3_TILE * H3_ROWB;    // K tile bytes (16 KiB)
 constexpr int H3_VTB = 2 * CH * H3_TILE * 2; // V tile bytes (16 KiB)
 constexpr int H3_PSHIFT = 7;                 // p = 2^(x - m + PSHIFT)
 constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by > 2^8
-#ifndef ATT_RING  // A/B knobs of the key-tile loop (tools/att_h3_bench.hip); defaults = production
-#define ATT_RING 1
-#endif
-#ifndef ATT_MPREF
-#define ATT_MPREF 0
-#endif
-#ifndef ATT_DMA_MID
-#define ATT_DMA_MID 0
-#endif
-#ifndef ATT_MUNI
-#define ATT_MUNI 0
-#endif
-#ifndef ATT_BAR
-#define ATT_BAR 1
-#endif
-#ifndef ATT_RFL
-#define ATT_RFL 1
-#endif
 constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8 (p * 2^-e stays >= 2^-24 of the sum)
 
 // The V-tile exponent for a tile whose max |v| is vmax: the largest e <= 8 with
@@ -224,12 +206,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const int N = g.N, Npad = g.Npad;
     // wave in an SGPR: every wave-uniform branch below (M orientation, active,
     // the barrier's count) is then a scalar branch, never an exec-masked one
-#if ATT_RFL
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5,
               l32 = lane & 31;
-#else
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-#endif
     const int q0 = qb * (NW * 32) + wave * 32;
     const int nst = (N + H3_TILE - 1) / H3_TILE;
     const int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
@@ -273,29 +251,27 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const uint32_t Nb = (uint32_t)N * 4;
 
     const float *vexp_b = vexp + (size_t)b * (Npad / H3_TILE);
-    // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys of tile key0.
-    // Returns the vector-memory instructions issued (the barrier's count).
-    auto load_m = [&](int key0, float (&mv)[16]) -> int {
+    // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys of tile key0
+    auto load_m = [&](int key0, float (&mv)[16]) {
         if constexpr (PACKED) {
             // the wave's 32 x 32 block IS one packed tile: (kt, qt) row-major when
-            // kt <= qt (rows = keys), else tile (qt, kt) read transposed (rows =
-            // queries).  One code path for both: element r of the lane's 16 sits at
-            // (r & 3) * sa + (r >> 2) * sb bytes past vo (uniform strides as the
-            // loads' scalar offsets), so no branch splits the load registers.
+            // kt <= qt (rows = keys: 16 loads, each 32 consecutive queries of a key
+            // row), else tile (qt, kt) read transposed (rows = queries: the lane's
+            // 16 keys are 4 runs of 4 in its query's row).  Scalar branch (q0 is
+            // wave-uniform in an SGPR).
             static_assert(MPACK_T == 32, "one packed tile per wave step");
             const int kt = key0 / MPACK_T, qt = q0 / MPACK_T;
-#if !ATT_MUNI
             const int kr = 4 * h, qr = l32;
-            if (kt <= qt) {
+            if (kt <= qt) {  // rows = keys
                 const uint32_t vo =
                     ((uint32_t)mpack_tile(kt, qt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(kr * MPACK_T + qr)) * 4;
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
                     mv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                           rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * (MPACK_T * 4), 0, 0));
-                return 16;
+                return;
             }
-            {
+            {  // rows = queries
                 const uint32_t vo =
                     ((uint32_t)mpack_tile(qt, kt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(qr * MPACK_T + kr)) * 4;
 #pragma unroll
@@ -304,18 +280,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
 #pragma unroll
                     for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[e];
                 }
-                return 4;
             }
-#endif
-            const bool rows_keys = kt <= qt;
-            const int tile_id = rows_keys ? mpack_tile(kt, qt, mnt) : mpack_tile(qt, kt, mnt);
-            const int in_tile = rows_keys ? (4 * h) * MPACK_T + l32 : l32 * MPACK_T + 4 * h;
-            const uint32_t vo = ((uint32_t)tile_id * (MPACK_T * MPACK_T) + (uint32_t)in_tile) * 4;
-            const int sa = rows_keys ? MPACK_T * 4 : 4, sb = rows_keys ? 8 * MPACK_T * 4 : 32;
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                mv[r] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo, (r & 3) * sa + (r >> 2) * sb, 0));
         } else {
             const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
 #pragma unroll
@@ -323,19 +288,17 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
                 mv[r] = __builtin_bit_cast(
                     float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb, 0, 0));
         }
-        return 16;
     };
 
-    // One key tile.  The M values were loaded one tile ahead (mv); after the
-    // softmax has consumed them, mid() queues the next tile's K / V DMA and its
-    // M loads (so the softmax waits only for loads a whole tile old).  K and V
-    // fragments are read two blocks ahead of their MFMAs (three register sets;
-    // sched_barrier keeps the compiler from sinking each read onto its MFMA).
-    auto tile = [&](const char *Kl, const char *Vl, int key0, float (&mv)[16], auto &&mid) {
+    // One key tile: M loads first (they land while QK^T runs), K and V fragments
+    // read two blocks ahead of their MFMAs (three register sets; sched_barrier
+    // keeps the compiler from sinking each read onto its MFMA).  (Prefetching M
+    // a whole tile ahead, or queueing the next DMA after the softmax, measured
+    // no faster: DESIGN.md §7.)
+    auto tile = [&](const char *Kl, const char *Vl, int key0) {
         const float ev = vexp_b[key0 / H3_TILE];  // wave-uniform
-#if !ATT_MPREF
+        float mv[16];
         load_m(key0, mv);
-#endif
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
         const char *krow = Kl + l32 * H3_ROWB;
@@ -345,21 +308,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             f[0] = *reinterpret_cast<const f16x8 *>(krow + 16 * ch);
             f[1] = *reinterpret_cast<const f16x8 *>(krow + CH * 2 + 16 * ch);
         };
-#if ATT_RING
         kread(0, kf[0]);
         kread(1, kf[1]);
-#endif
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-#if ATT_RING
             if (j + 2 < 8) kread(j + 2, kf[(j + 2) % 3]);
             S = mfma_h3(kf[j % 3][0], kf[j % 3][1], qh[j], ql[j], S);
             __builtin_amdgcn_sched_barrier(0);
-#else
-            f16x8 kk[2];
-            kread(j, kk);
-            S = mfma_h3(kk[0], kk[1], qh[j], ql[j], S);
-#endif
         }
         float p[16];
         float mx = -INFINITY;
@@ -402,7 +357,6 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             split8x(v, ph[s], pl[s]);
         }
         l_run += ldexpf(psum, (int)ev);
-        mid();
         // O[query][4 l32 + t] += sum_key P[query][key] V[key][4 l32 + t]
         const int sw = (l32 >> 2) & 3;
         f16x8 vf[3][2];
@@ -412,77 +366,36 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             f[0] = *reinterpret_cast<const f16x8 *>(vrow + 16 * ch);
             f[1] = *reinterpret_cast<const f16x8 *>(vrow + CH * H3_TILE * 2 + 16 * ch);
         };
-#if ATT_RING
         vread(0, vf[0]);
         vread(1, vf[1]);
-#endif
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-#if ATT_RING
             if (i + 2 < 8) vread(i + 2, vf[(i + 2) % 3]);
             O[i >> 1] = mfma_h3(ph[i & 1], pl[i & 1], vf[i % 3][0], vf[i % 3][1], O[i >> 1]);
             __builtin_amdgcn_sched_barrier(0);
-#else
-            f16x8 vv[2];
-            vread(i, vv);
-            O[i >> 1] = mfma_h3(ph[i & 1], pl[i & 1], vv[0], vv[1], O[i >> 1]);
-#endif
         }
     };
 
-    // End of a tile: this wave's DMA of the next tile has landed (all but the nm
-    // youngest vector-memory ops -- the next tile's M loads, queued after the
-    // DMA -- are done) and its LDS reads returned; then the workgroup barrier.
-    // (__syncthreads would drain the M prefetch too.)
-    // The waits are s_waitcnt builtins (not asm) so the compiler's counter model
-    // learns that the DMA is done and adds no vmcnt(0) before the next tile's LDS
-    // reads.  Immediates (gfx9 simm16): vmcnt[3:0] | expcnt << 4 | lgkmcnt << 8 |
-    // vmcnt[5:4] << 14.
-    auto sync = [&](int nm) {
-#if !ATT_BAR
-        __syncthreads();
-        return;
-#endif
-        if (nm == 4)
-            __builtin_amdgcn_s_waitcnt(0x0074);  // vmcnt(4)
-        else if (nm == 16)
-            __builtin_amdgcn_s_waitcnt(0x4070);  // vmcnt(16) expcnt(7) lgkmcnt(0)
-        else
-            __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0)
+    // End of a tile: this wave's DMA of the next tile has landed and its LDS
+    // reads returned, then the workgroup barrier -- as an s_waitcnt builtin
+    // (not asm, not __syncthreads) so the compiler's counter model learns that
+    // the DMA is done and adds no vmcnt(0) before the next tile's LDS reads.
+    // Immediate (gfx9 simm16): vmcnt[3:0] | expcnt(7) << 4 | lgkmcnt(0) << 8.
+    auto sync = [&] {
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
     };
 
-    float mv[16];
-    if (st0 < st1) {
-        stage(st0, 0);
-#if ATT_MPREF
-        if (active) load_m(st0 * H3_TILE, mv);
-#endif
-    }
-    sync(0);
+    if (st0 < st1) stage(st0, 0);
+    sync();
     for (int st = st0; st < st1; ++st) {
         const int slot = (st - st0) & 1;
-        int nm = 0;
-#if !ATT_DMA_MID
         if (st + 1 < st1) stage(st + 1, slot ^ 1);
-#endif
-        auto next = [&] {
-            if (st + 1 < st1) {
-#if ATT_DMA_MID
-                stage(st + 1, slot ^ 1);
-#endif
-#if ATT_MPREF
-                if (active) nm = load_m((st + 1) * H3_TILE, mv);
-#endif
-            }
-        };
         if (active) {
             const char *base = h3smem + slot * (H3_KTB + H3_VTB);
-            tile(base, base + H3_KTB, st * H3_TILE, mv, next);
-        } else {
-            next();
+            tile(base, base + H3_KTB, st * H3_TILE);
         }
-        sync(nm);
+        sync();
     }
     if (!active) return;
 
