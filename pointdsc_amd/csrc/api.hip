@@ -390,7 +390,7 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
         HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, vexp, s));
     }
     HIPCHK(launch_attention(qs, ks, vs, vexp, M, false, f32, B, N, Npad, ns, op, ml, s));
-    HIPCHK(launch_attn_combine(op, ml, B, N, Npad, ns, msg, s));
+    HIPCHK(launch_attn_combine(op, ml, f32, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
 

@@ -25,15 +25,21 @@
 // softmax is sensitive to.
 //
 // HBM layouts (written by the pointwise kernels' epilogues, encoder.hip, or
-// by split_qkv_kernel for the standalone API), per pair, Npad rows:
-//   Qs [Npad][2][128] fp16   row = query; [0] = hi, [1] = lo; channels in
-//                            qk_pos order (bits 2 and 3 of the index swapped)
-//   Ks [Npad][2][128] fp16   as Qs, and each 16-B chunk c of a row stored at
-//                            chunk c ^ (row & 15) (conflict-free LDS reads)
-//   Vs [Npad/32][2][128][32] per 32-key tile: hi plane, lo plane; plane row
-//                            rho(c) = 32 (c & 3) + (c >> 2); keys in v_keypos
-//                            order; 16-B chunk c of a row at c ^ ((rho >> 2) & 3)
+// by split_qkv_kernel for the standalone API), per pair, in 32-row tiles of
+// 16 KiB made of 16 "fragment blocks" of 1 KiB: block (f, plane) holds, for
+// each lane (h, n) of a wave in lane order, the 16 B (8 fp16) that lane feeds
+// the MFMA as operand fragment f -- so a producer's store of one fragment and
+// a consumer's load of it (or LDS-DMA + ds_read) are one contiguous 1 KiB:
+//   Qs, Ks  fragment j (k-step, 0..7), lane (h, n): row n of the tile,
+//           positions 16 j + 8h .. +7 of the row in qk_pos order (bits 2 and 3
+//           of the channel index swapped); plane 0 = hi, 1 = lo
+//   Vs      fragment i = 2t + s, lane (h, n): channel 32 t + n, the tile's
+//           keys at v_keypos positions 16 s + 8h .. +7
 // Each layout equals the fp32 tensor's size (4 B per element).
+// The partial outputs (opart) use the same tiling for fp32: per 32-query tile
+// 16 blocks (2 ks + g) of 64 lanes x 4 floats, lane (h, n) = query n,
+// qk_pos positions 16 ks + 8h + 4g .. +3 (h3_opart_off) -- the k-step
+// fragments of the message layer that consumes them.
 //
 // Work decomposition (as attention.hpp): a workgroup = NW waves x 32 queries
 // of one pair and a contiguous split of 32-key tiles; K and V tiles (16 KiB
@@ -41,8 +47,11 @@
 // wave and tile:
 //   S^T = K Q^T      8 k-steps x 3 MFMA 32x32x16 (lane <-> query)
 //   logits, online softmax with a lazily re-based max (as attention.hpp)
-//   O  += P V        the S^T accumulator registers 8s..8s+7 ARE the A operand
-//                    of k-step s (key order = v_keypos), 4 channel tiles x 2 x 3 MFMA
+//   O^T += V^T P^T   the S^T accumulator registers 8s..8s+7 ARE the B operand
+//                    of k-step s (key order = v_keypos), 4 channel tiles x 2 x 3
+//                    MFMA; lane <-> query again, so the softmax re-scale is a
+//                    per-lane multiply and O^T registers 8u..8u+7 of tile t are
+//                    the consuming layer's k-step 2t + u fragment
 #pragma once
 #include "pdsc_internal.hpp"
 
@@ -71,19 +80,27 @@ PDSC_DEV int h3_vexp(float vmax) {
 PDSC_DEV constexpr int qk_pos(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
 // key (0..31 within a tile) -> position in a Vs plane row: swap bits 2 and 3
 PDSC_DEV constexpr int v_keypos(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
-// channel -> row of a Vs plane
-PDSC_DEV constexpr int v_rho(int c) { return 32 * (c & 3) + (c >> 2); }
+// Fragment-block tiling (above): 32 rows x 128 channels x (hi, lo) per tile;
+// element offset of (fragment f, plane, lane) in fp16 units within the tile.
+constexpr int H3_TILE_H = 2 * CH * H3_TILE;  // fp16 per tile (8192)
+PDSC_DEV constexpr int h3_frag(int f, int plane, int lane) { return ((2 * f + plane) * 64 + lane) * 8; }
 
 // element offsets (in fp16 units) inside one pair's buffers
-PDSC_DEV size_t qs_off(int row, int half, int c) { return (size_t)row * 2 * CH + half * CH + qk_pos(c); }
-PDSC_DEV size_t ks_off(int row, int half, int c) {
+PDSC_DEV size_t qs_off(int row, int half, int c) {
     const int p = qk_pos(c);
-    return (size_t)row * 2 * CH + half * CH + 8 * ((p >> 3) ^ (row & 15)) + (p & 7);
+    return (size_t)(row >> 5) * H3_TILE_H + h3_frag(p >> 4, half, 32 * ((p >> 3) & 1) + (row & 31)) + (p & 7);
 }
+PDSC_DEV size_t ks_off(int row, int half, int c) { return qs_off(row, half, c); }
 PDSC_DEV size_t vs_off(int key, int half, int c) {
-    const int rho = v_rho(c), kp = v_keypos(key & 31);
-    return (size_t)(key >> 5) * (2 * CH * H3_TILE) + (size_t)half * CH * H3_TILE + rho * H3_TILE +
-           8 * ((kp >> 3) ^ ((rho >> 2) & 3)) + (kp & 7);
+    const int kp = v_keypos(key & 31);
+    return (size_t)(key >> 5) * H3_TILE_H + h3_frag(2 * (c >> 5) + (kp >> 4), half, 32 * ((kp >> 3) & 1) + (c & 31)) +
+           (kp & 7);
+}
+// fp32 offset of (row, channel c) in one (pair, split)'s opart of Npad rows
+PDSC_DEV size_t h3_opart_off(int row, int c) {
+    const int p = qk_pos(c);
+    return (size_t)(row >> 5) * (H3_TILE * CH) + ((2 * (p >> 4) + ((p >> 2) & 1)) * 64 + 32 * ((p >> 3) & 1) + (row & 31)) * 4 +
+           (p & 3);
 }
 
 // x = hi + lo (fp16 pair).  The empty asm pins x as the rounded fp32 value:
@@ -220,14 +237,14 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const size_t mper = PACKED ? (size_t)mnt * (mnt + 1) / 2 * MPACK_T * MPACK_T : (size_t)N * N;
     const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M + (size_t)b * mper, (uint32_t)(mper * 4u));
 
-    // this lane's query: 8 k-steps x (hi, lo) fragments, chunk 2j + h of its row
+    // this lane's query: 8 k-steps x (hi, lo) fragments (16 coalesced 1-KiB loads)
     f16x8 qh[8], ql[8];
     {
-        const char *qrow = reinterpret_cast<const char *>(Qs + ((size_t)b * Npad + min(qq, Npad - 1)) * 2 * CH);
+        const _Float16 *qt = Qs + (size_t)b * Npad * 2 * CH + (size_t)(min(q0, Npad - 32) >> 5) * H3_TILE_H;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            qh[j] = *reinterpret_cast<const f16x8 *>(qrow + 16 * (2 * j + h));
-            ql[j] = *reinterpret_cast<const f16x8 *>(qrow + CH * 2 + 16 * (2 * j + h));
+            qh[j] = *reinterpret_cast<const f16x8 *>(qt + h3_frag(j, 0, lane));
+            ql[j] = *reinterpret_cast<const f16x8 *>(qt + h3_frag(j, 1, lane));
         }
     }
 
@@ -301,12 +318,10 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
         load_m(key0, mv);
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
-        const char *krow = Kl + l32 * H3_ROWB;
         f16x8 kf[3][2];
         auto kread = [&](int j, f16x8(&f)[2]) {
-            const int ch = (2 * j + h) ^ (l32 & 15);
-            f[0] = *reinterpret_cast<const f16x8 *>(krow + 16 * ch);
-            f[1] = *reinterpret_cast<const f16x8 *>(krow + CH * 2 + 16 * ch);
+            f[0] = *reinterpret_cast<const f16x8 *>(Kl + 2 * h3_frag(j, 0, lane));
+            f[1] = *reinterpret_cast<const f16x8 *>(Kl + 2 * h3_frag(j, 1, lane));
         };
         kread(0, kf[0]);
         kread(1, kf[1]);
@@ -334,11 +349,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             m_run = m_new;
             l_run *= alpha;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float a = __shfl(alpha, acc_row(r, h));
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) O[t][r] *= a;
-            }
+                for (int r = 0; r < 16; ++r) O[t][r] *= alpha;  // lane = query
         }
         const float mb = m_run - (float)H3_PSHIFT + ev;
         float psum = 0.0f;
@@ -357,21 +370,21 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
             split8x(v, ph[s], pl[s]);
         }
         l_run += ldexpf(psum, (int)ev);
-        // O[query][4 l32 + t] += sum_key P[query][key] V[key][4 l32 + t]
-        const int sw = (l32 >> 2) & 3;
+        // O^T[32 t + m][query] += sum_key V[key][32 t + m] P[query][key]
         f16x8 vf[3][2];
-        auto vread = [&](int i, f16x8(&f)[2]) {  // block i = (t, s) = (i / 2, i % 2)
-            const char *vrow = Vl + (32 * (i >> 1) + l32) * (H3_TILE * 2);
-            const int ch = (2 * (i & 1) + h) ^ sw;
-            f[0] = *reinterpret_cast<const f16x8 *>(vrow + 16 * ch);
-            f[1] = *reinterpret_cast<const f16x8 *>(vrow + CH * H3_TILE * 2 + 16 * ch);
+        auto vread = [&](int i, f16x8(&f)[2]) {  // fragment i = (t, s) = (i / 2, i % 2)
+            f[0] = *reinterpret_cast<const f16x8 *>(Vl + 2 * h3_frag(i, 0, lane));
+            f[1] = *reinterpret_cast<const f16x8 *>(Vl + 2 * h3_frag(i, 1, lane));
         };
         vread(0, vf[0]);
         vread(1, vf[1]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             if (i + 2 < 8) vread(i + 2, vf[(i + 2) % 3]);
-            O[i >> 1] = mfma_h3(ph[i & 1], pl[i & 1], vf[i % 3][0], vf[i % 3][1], O[i >> 1]);
+            // the three products in the order of P V's mfma_h3 (pl.vh, ph.vl, ph.vh)
+            f32x16 o = mfma_h(vf[i % 3][0], pl[i & 1], O[i >> 1]);
+            o = mfma_h(vf[i % 3][1], ph[i & 1], o);
+            O[i >> 1] = mfma_h(vf[i % 3][0], ph[i & 1], o);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -401,12 +414,14 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
 
     l_run += __shfl_xor(l_run, 32);
     const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
-    float *Ob = opart + obase * CH;
+    // registers 8u + 4g .. +3 of tile t = fragment block 2 (2t + u) + g (16 coalesced 1-KiB stores)
+    float *Ob = opart + obase * CH + (size_t)(q0 >> 5) * (H3_TILE * CH) + 4 * lane;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = q0 + acc_row(r, h);
-        *reinterpret_cast<f32x4 *>(Ob + (size_t)row * CH + 4 * l32) = f32x4{O[0][r], O[1][r], O[2][r], O[3][r]};
-    }
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4 *>(Ob + (4 * t + q) * 256) =
+                f32x4{O[t][4 * q], O[t][4 * q + 1], O[t][4 * q + 2], O[t][4 * q + 3]};
     if (h == 0) {
         // partial max in natural-log units (the p's carry the 2^PSHIFT factor)
         ml[(obase + qq) * 2] = (m_run - (float)H3_PSHIFT) * 0.6931471805599453f;

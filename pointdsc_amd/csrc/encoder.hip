@@ -196,6 +196,10 @@ hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int 
 }
 
 // Combine the split partials of one row segment: msg = sum_s O_s e^{m_s-m*} / sum_s l_s e^{m_s-m*}.
+// Channels d0 .. d0+15 (d0 % 16 == 0) as 4 runs of 4: opart rows [Npad][CH]
+// (F32 attention) or the fragment-block tiling (H3, attention_h3.hpp: run a
+// of the 16 sits in block 2 (d0/16) + (a >> 1), lane half a & 1).
+template <bool F32>
 PDSC_DEV void combine16(const float *__restrict__ opart, const float *__restrict__ ml, int b,
                         int nsplit, int Npad, int row, int d0, float out[16]) {
     float mstar = -INFINITY;
@@ -206,9 +210,12 @@ PDSC_DEV void combine16(const float *__restrict__ opart, const float *__restrict
         const size_t base = (size_t)(b * nsplit + s) * Npad + row;
         const float w = expf(ml[base * 2] - mstar);
         L += w * ml[base * 2 + 1];
-        const f32x4 *src = reinterpret_cast<const f32x4 *>(opart + base * CH + d0);
+        const float *ob = opart + (base - row) * CH;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] += w * src[i];
+        for (int i = 0; i < 4; ++i) {
+            const size_t o = F32 ? (size_t)row * CH + d0 + 4 * i : h3_opart_off(row, d0 + 4 * i);
+            acc[i] += w * *reinterpret_cast<const f32x4 *>(ob + o);
+        }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -216,6 +223,7 @@ PDSC_DEV void combine16(const float *__restrict__ opart, const float *__restrict
         for (int e = 0; e < 4; ++e) out[4 * i + e] = acc[i][e] / L;
 }
 
+template <bool F32>
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float *__restrict__ opart,
                                                            const float *__restrict__ ml, int N,
                                                            int Npad, int nsplit,
@@ -224,16 +232,20 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float *__restri
     const int row = blockIdx.x * 32 + (threadIdx.x >> 3), d0 = (threadIdx.x & 7) * 16;
     if (row >= N) return;
     float out[16];
-    combine16(opart, ml, b, nsplit, Npad, row, d0, out);
+    combine16<F32>(opart, ml, b, nsplit, Npad, row, d0, out);
     f32x4 *dst = reinterpret_cast<f32x4 *>(msg + ((size_t)b * N + row) * CH + d0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[i] = f32x4{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
 }
 
-hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
+hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, int B, int N, int Npad,
                                int nsplit, float *msg, hipStream_t s) {
-    hipLaunchKernelGGL(attn_combine_kernel, dim3((N + 31) / 32, B), dim3(256), 0, s, opart, ml, N,
-                       Npad, nsplit, msg);
+    if (f32)
+        hipLaunchKernelGGL(attn_combine_kernel<true>, dim3((N + 31) / 32, B), dim3(256), 0, s, opart, ml, N, Npad,
+                           nsplit, msg);
+    else
+        hipLaunchKernelGGL(attn_combine_kernel<false>, dim3((N + 31) / 32, B), dim3(256), 0, s, opart, ml, N, Npad,
+                           nsplit, msg);
     return hipGetLastError();
 }
 
@@ -409,7 +421,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
     }
     const float inv = pk[off.scale];
     if constexpr (MODE == SPLIT_V) {
-        const int c = ct * 32 + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
+        const int c = ct * 32 + l32;
         const float bias = pk[off.bias + c];
         int ev[NRT];
 #pragma unroll
@@ -431,7 +443,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
         }
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
-            _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * (2 * CH * H3_TILE) + rho * H3_TILE;
+            _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * H3_TILE_H;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 f16x8 hi, lo;
@@ -442,9 +454,8 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
                     hi[e] = a;
                     lo[e] = b;
                 }
-                const int chk = (2 * s + h) ^ sw;
-                *reinterpret_cast<f16x8 *>(tile + 8 * chk) = hi;
-                *reinterpret_cast<f16x8 *>(tile + CH * H3_TILE + 8 * chk) = lo;
+                *reinterpret_cast<f16x8 *>(tile + h3_frag(2 * ct + s, 0, lane)) = hi;
+                *reinterpret_cast<f16x8 *>(tile + h3_frag(2 * ct + s, 1, lane)) = lo;
             }
         }
     } else {
@@ -453,8 +464,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
         for (int r = 0; r < 16; ++r) bias[r] = pk[off.bias + ct * 32 + acc_row(r, h)];
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
-            const int row = p0 + 32 * i + l32;
-            _Float16 *drow = dst + (size_t)row * 2 * CH;
+            _Float16 *tile = dst + (size_t)((p0 >> 5) + i) * H3_TILE_H;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 f16x8 hi, lo;
@@ -465,10 +475,8 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
                     hi[e] = a;
                     lo[e] = b;
                 }
-                int chk = 4 * ct + 2 * s + h;
-                if (MODE == SPLIT_K) chk ^= row & 15;
-                *reinterpret_cast<f16x8 *>(drow + 8 * chk) = hi;
-                *reinterpret_cast<f16x8 *>(drow + CH + 8 * chk) = lo;
+                *reinterpret_cast<f16x8 *>(tile + h3_frag(2 * ct + s, 0, lane)) = hi;
+                *reinterpret_cast<f16x8 *>(tile + h3_frag(2 * ct + s, 1, lane)) = lo;
             }
         }
     }
@@ -591,7 +599,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
-template <int PTT>
+template <int PTT, bool F32>
 PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restrict__ ml, int b,
                            int nsplit, int Npad, int p0, float *X, int tid) {
     constexpr int TPR = 256 / PTT, NH = 8 / TPR;  // threads per row, 16-channel pieces per thread
@@ -600,7 +608,7 @@ PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restr
     for (int half = 0; half < NH; ++half) {
         const int d0 = (tid % TPR) * (16 * NH) + half * 16;
         float out[16];
-        combine16(opart, ml, b, nsplit, Npad, p0 + p, d0, out);
+        combine16<F32>(opart, ml, b, nsplit, Npad, p0 + p, d0, out);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             *reinterpret_cast<f32x4 *>(X + p * S132 + d0 + 4 * i) =
@@ -633,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
-    combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
+    combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
@@ -653,7 +661,7 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
     const int nrows = min(PTT, N - p0);
-    combine_tile<PTT>(opart, ml, b, nsplit, Npad, p0, XA, tid);
+    combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     // XB = corr_features rows
@@ -890,9 +898,11 @@ PDSC_DEV void w2_epilogue(f32x16 (&acc)[OUT / 32], float inv, const float *cf, c
 }
 
 // Combine the split partials of this lane's point into the k-step fragments of
-// the 128 message channels (as combine16: sum_s w_s O_s / sum_s w_s l_s).
+// the 128 message channels (as combine16: sum_s w_s O_s / sum_s w_s l_s).  The
+// partials are in the fragment-block tiling (attention_h3.hpp): k-step ks is
+// blocks 2 ks and 2 ks + 1 at this lane, 16 coalesced 1-KiB loads per split.
 PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restrict__ ml, int b, int nsplit, int Npad,
-                         int row, f16x8 *xh, f16x8 *xl, int h) {
+                         int row, f16x8 *xh, f16x8 *xl, int lane) {
     float mstar = -INFINITY;
     for (int s = 0; s < nsplit; ++s) mstar = fmaxf(mstar, ml[((size_t)(b * nsplit + s) * Npad + row) * 2]);
     float L = 0.0f;
@@ -903,12 +913,9 @@ PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restric
         const size_t base = (size_t)(b * nsplit + s) * Npad + row;
         const float w = expf(ml[base * 2] - mstar);
         L += w * ml[base * 2 + 1];
-        const float *src = opart + base * CH + 4 * h;
+        const float *src = opart + (base - (row & 31)) * CH + 4 * lane;  // the tile's first block
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            acc[2 * ks] += w * *reinterpret_cast<const f32x4 *>(src + 16 * ks);
-            acc[2 * ks + 1] += w * *reinterpret_cast<const f32x4 *>(src + 16 * ks + 8);
-        }
+        for (int i = 0; i < 16; ++i) acc[i] += w * *reinterpret_cast<const f32x4 *>(src + 256 * i);
     }
     const float rl = 1.0f / L;  // the softmax denominator once (the reference divides e by its sum first)
 #pragma unroll
@@ -944,13 +951,13 @@ PDSC_DEV void w2_store_row(float *__restrict__ featL, int row, int h, const f32x
         for (int q = 0; q < 4; ++q) dst[4 * t + q] = f32x4{y[t][4 * q], y[t][4 * q + 1], y[t][4 * q + 2], y[t][4 * q + 3]};
 }
 
-// Q / K outputs (transposed, bias only; 16 stores) in the attention_h3 row
-// layouts: registers 8u .. 8u+7 of tile t = qk_pos positions 32t + 16u + 8h .. +7.
-template <bool SWZ>
+// Q / K outputs (transposed, bias only) in the attention_h3 fragment-block
+// tiling: registers 8u .. 8u+7 of tile t = fragment 2t + u of this lane (qk_pos
+// positions 32t + 16u + 8h .. +7 of its point): 16 coalesced 1-KiB stores.
 PDSC_DEV void w2_store_qk(const f32x16 (&acc)[4], float inv, const float *bias, _Float16 *__restrict__ dst, int row,
                           int lane) {
     const int h = lane >> 5;
-    _Float16 *drow = dst + (size_t)row * 2 * CH;
+    _Float16 *dtile = dst + (size_t)(row >> 5) * H3_TILE_H;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -962,16 +969,15 @@ PDSC_DEV void w2_store_qk(const f32x16 (&acc)[4], float inv, const float *bias, 
             for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(acc[t][8 * u + e], inv, e < 4 ? b0[e] : b1[e - 4]);
             f16x8 hi, lo;
             split8v(v, hi, lo);
-            int chk = 4 * t + 2 * u + h;
-            if (SWZ) chk ^= row & 15;
-            *reinterpret_cast<f16x8 *>(drow + 8 * chk) = hi;
-            *reinterpret_cast<f16x8 *>(drow + CH + 8 * chk) = lo;
+            *reinterpret_cast<f16x8 *>(dtile + h3_frag(2 * t + u, 0, lane)) = hi;
+            *reinterpret_cast<f16x8 *>(dtile + h3_frag(2 * t + u, 1, lane)) = lo;
         }
 }
 
-// V output (untransposed: lane l32 <-> channel 32t + l32, register r <-> point
-// acc_row(r, h) of the wave's key tile) into the tile's V planes, scaled by the
-// tile's 2^vexp (the tile's max |v| is wave-local here).
+// V output (untransposed: lane l32 <-> channel 32t + l32, registers 8s .. 8s+7
+// <-> the key tile's v_keypos positions 16s + 8h .. +7) = fragment 2t + s of
+// this lane in the V tiling, scaled by the tile's 2^vexp (the tile's max |v| is
+// wave-local here): 16 coalesced 1-KiB stores.
 PDSC_DEV void w2_store_v(f32x16 (&acc)[4], float inv, const float *bias, _Float16 *__restrict__ Vt,
                          float *__restrict__ vexp_t, int lane) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -989,8 +995,6 @@ PDSC_DEV void w2_store_v(f32x16 (&acc)[4], float inv, const float *bias, _Float1
     if (lane == 0) *vexp_t = (float)ev;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const int c = 32 * t + l32, rho = v_rho(c), sw = (rho >> 2) & 3;
-        _Float16 *prow = Vt + rho * H3_TILE;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             float v[8];
@@ -998,9 +1002,8 @@ PDSC_DEV void w2_store_v(f32x16 (&acc)[4], float inv, const float *bias, _Float1
             for (int e = 0; e < 8; ++e) v[e] = ldexpf(acc[t][8 * s + e], ev);
             f16x8 hi, lo;
             split8v(v, hi, lo);
-            const int chk = (2 * s + h) ^ sw;
-            *reinterpret_cast<f16x8 *>(prow + 8 * chk) = hi;
-            *reinterpret_cast<f16x8 *>(prow + CH * H3_TILE + 8 * chk) = lo;
+            *reinterpret_cast<f16x8 *>(Vt + h3_frag(2 * t + s, 0, lane)) = hi;
+            *reinterpret_cast<f16x8 *>(Vt + h3_frag(2 * t + s, 1, lane)) = lo;
         }
     }
 }
@@ -1034,11 +1037,11 @@ PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const W2Sched 
         w2_store_row(featL, row, h, acc);
     }
     w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
-    if (active) w2_store_qk<false>(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
+    if (active) w2_store_qk(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
     w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
-    if (active) w2_store_qk<true>(acc, sk, cf + W2CoefQKV::k, K, row, lane);
+    if (active) w2_store_qk(acc, sk, cf + W2CoefQKV::k, K, row, lane);
     w2_layer<CH, CH, false, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
-    if (active) w2_store_v(acc, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * (2 * CH * H3_TILE), vexp + (row >> 5), lane);
+    if (active) w2_store_v(acc, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * H3_TILE_H, vexp + (row >> 5), lane);
 }
 
 #define PW2_PROLOGUE                                                                              \
@@ -1106,7 +1109,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const 
     w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
     w2_coef(cf + CF6, pk, m.fc6, CH, tid);
     f16x8 xh[8], xl[8];
-    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
+    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
     __syncthreads();
     f32x16 a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
     w2_coef(cf + CC2, pk, c2, CLS, tid);
     for (int i = tid; i < CLS; i += PW2_W * 64) cf[CC4 + i] = pk[c4w + i];
     f16x8 xh[8], xl[8];
-    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, h);
+    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
     __syncthreads();
     f32x16 a1[1], a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];

@@ -152,8 +152,8 @@ __global__ void split_rows_kernel(const float *__restrict__ x, size_t rows, _Flo
     const int c = (int)(i % CH);
     _Float16 hi, lo;
     split_h(x[i], hi, lo);
-    out[qs_off((int)0, 0, c) + row * 2 * CH] = hi;
-    out[qs_off((int)0, 1, c) + row * 2 * CH] = lo;
+    out[(size_t)row * 2 * CH + qk_pos(c)] = hi;
+    out[(size_t)row * 2 * CH + CH + qk_pos(c)] = lo;
 }
 
 hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s) {

@@ -132,7 +132,9 @@ hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, 
                              float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s);
 hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 
-// Attention partials for one layer: opart [B][nsplit][Npad][CH], ml [B][nsplit][Npad][2].
+// Attention partials for one layer: opart [B][nsplit][Npad x CH], ml [B][nsplit][Npad][2];
+// opart rows [Npad][CH] for f32, the fragment-block tiling of attention_h3.hpp
+// (h3_opart_off) for H3.
 int attention_nsplit(int B, int N, bool f32);
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
 // or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
@@ -147,7 +149,7 @@ hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hip
 hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int B, int N, int ld, int Npad,
                             _Float16 *qs, _Float16 *ks, _Float16 *vs, float *vexp, hipStream_t s);
 // Combine partials -> msg [B][Npad][CH] (used by the standalone attention API).
-hipError_t launch_attn_combine(const float *opart, const float *ml, int B, int N, int Npad,
+hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, int B, int N, int Npad,
                                int nsplit, float *msg, hipStream_t s);
 
 // Pointwise chains (one workgroup per PT points); q, k, v in launch_attention's layouts.
