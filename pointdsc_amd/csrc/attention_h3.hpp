@@ -204,7 +204,7 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
 // PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
 // vexp: [B][Npad/32] V-tile exponents (see above).
 template <int NW, bool XCD, bool PACKED>
-__global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
+__global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
     float *__restrict__ ml) {

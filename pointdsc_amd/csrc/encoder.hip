@@ -930,25 +930,27 @@ PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restric
     }
 }
 
-// This lane's 64 fp32 values of a 128-channel row (featL: [Npad][2][64], the
-// lane-register order of a transposed 128-output layer): 16 x 16 B each way.
-PDSC_DEV void w2_load_row(const float *__restrict__ featL, int row, int h, f32x16 (&y)[4]) {
-    const f32x4 *src = reinterpret_cast<const f32x4 *>(featL + ((size_t)row * 2 + h) * 64);
+// This lane's 64 fp32 values of a 128-channel row.  featL keeps the lane-register
+// order of a transposed 128-output layer in the fragment-block tiling of the
+// attention partials (per 32-row tile, block 4t + q = registers 4q .. 4q+3 of
+// tile t for the 64 lanes): 16 coalesced 1-KiB accesses each way.
+PDSC_DEV void w2_load_row(const float *__restrict__ featL, int row, int lane, f32x16 (&y)[4]) {
+    const f32x4 *src = reinterpret_cast<const f32x4 *>(featL + (size_t)(row >> 5) * (32 * CH)) + lane;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const f32x4 v = src[4 * t + q];
+            const f32x4 v = src[64 * (4 * t + q)];
 #pragma unroll
             for (int e = 0; e < 4; ++e) y[t][4 * q + e] = v[e];
         }
 }
-PDSC_DEV void w2_store_row(float *__restrict__ featL, int row, int h, const f32x16 (&y)[4]) {
-    f32x4 *dst = reinterpret_cast<f32x4 *>(featL + ((size_t)row * 2 + h) * 64);
+PDSC_DEV void w2_store_row(float *__restrict__ featL, int row, int lane, const f32x16 (&y)[4]) {
+    f32x4 *dst = reinterpret_cast<f32x4 *>(featL + (size_t)(row >> 5) * (32 * CH)) + lane;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dst[4 * t + q] = f32x4{y[t][4 * q], y[t][4 * q + 1], y[t][4 * q + 2], y[t][4 * q + 3]};
+        for (int q = 0; q < 4; ++q) dst[64 * (4 * t + q)] = f32x4{y[t][4 * q], y[t][4 * q + 1], y[t][4 * q + 2], y[t][4 * q + 3]};
 }
 
 // Q / K outputs (transposed, bias only) in the attention_h3 fragment-block
@@ -1034,7 +1036,7 @@ PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const W2Sched 
     w2_layer<CH, CH, true>(P, pk, S, xh, xl, acc, active, wave, lane);
     if (active) {
         w2_epilogue<CH, EPI_BN_RELU>(acc, sp, cf + W2CoefQKV::pcn, nullptr, yh, yl, lane);
-        w2_store_row(featL, row, h, acc);
+        w2_store_row(featL, row, lane, acc);
     }
     w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
     if (active) w2_store_qk(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
@@ -1118,7 +1120,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const 
     w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
-        w2_load_row(featL + boff, row, h, res);  // the residual: lands during fc6's MFMAs
+        w2_load_row(featL + boff, row, lane, res);  // the residual: lands during fc6's MFMAs
     }
     w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);
@@ -1152,7 +1154,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
     w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
-        w2_load_row(featL + boff, row, h, res);
+        w2_load_row(featL + boff, row, lane, res);
     }
     w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     const bool in = row < N;

@@ -11,6 +11,9 @@
 #include "attention_h3.hpp"
 
 using namespace pdsc;
+#ifndef NWV
+#define NWV 4  // waves (x 32 queries) per workgroup
+#endif
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -43,7 +46,7 @@ __global__ void fill_f(float *p, size_t n, unsigned seed) {
 int main(int argc, char **argv) {
     const int B = argc > 1 ? atoi(argv[1]) : 128, N = argc > 2 ? atoi(argv[2]) : 1000;
     const int reps = argc > 3 ? atoi(argv[3]) : 20;
-    const AttnGridH3 g = attention_h3_grid<4>(B, N, 512);
+    const AttnGridH3 g = attention_h3_grid<NWV>(B, N, 512);
     const size_t rows = (size_t)B * g.Npad * CH * 2, mper = mpack_floats(N);
     _Float16 *Q, *K, *V;
     float *M, *vexp, *op, *ml;
@@ -59,12 +62,12 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(fill_h, dim3((rows + 255) / 256), dim3(256), 0, 0, V, rows, 3u, 1.0f);
     hipLaunchKernelGGL(fill_f, dim3((B * mper + 255) / 256), dim3(256), 0, 0, M, (size_t)B * mper, 4u);
     CK(hipMemset(vexp, 0, (size_t)B * (g.Npad / 32) * 4));
-    const size_t lds = attention_h3_lds_bytes<4>();
+    const size_t lds = attention_h3_lds_bytes<NWV>();
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     auto launch = [&] {
-        hipLaunchKernelGGL((attention_h3_kernel<4, true, true>), dim3(g.B * g.nqb * g.nsplit), dim3(256), lds, 0, Q,
+        hipLaunchKernelGGL((attention_h3_kernel<NWV, true, true>), dim3(g.B * g.nqb * g.nsplit), dim3(NWV * 64), lds, 0, Q,
                            K, V, vexp, M, g, op, ml);
     };
     for (int i = 0; i < 3; ++i) launch();
