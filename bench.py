@@ -332,24 +332,33 @@ def main():
 
     result = None
     if rank == 0:
-        # ---- dominant kernel: attention, HIP events around each launch in the timed region
+        # ---- dominant kernel: the attention (fused with the following pointwise chain
+        # where the encoder plan says so), HIP events around each launch in the timed region
         att_ms = sum(att_times) / len(att_times)
-        flops = P * 4.0 * N * N * 128
-        achieved = flops / (att_ms * 1e-3) / 1e12
-        npad, nsplit = ctypes.c_int32(), ctypes.c_int32()
+        npad, nsplit, fused = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(L.pdsc_attention_layout(P, N, 0, ctypes.byref(npad), ctypes.byref(nsplit)), "attention_layout")
-        att_prof = profiled("attention_h3_kernel<4>", P * (npad.value // 128) * nsplit.value * 256)
-        roofline = {"kernel": "attention_h3_kernel<4,xcd>", "bound": "mfma",
+        _lib.check(L.pdsc_encoder_plan(P, N, 0, ctypes.byref(fused)), "encoder_plan")
+        grid = P * (npad.value // 128) * nsplit.value * 256
+        if fused.value:
+            # attention 4 N^2 C + chain 2 x (fc0 128x64 + fc3 64x64 + fc6 64x128 + PointCN/Q/K/V 4 x 128x128) per point
+            flops = P * (4.0 * N * N * 128 + 2.0 * 86016 * N)
+            kname, kdesc, n_launch = "attn_pw2_kernel<1>", "attn_pw2_kernel (attention_l + pointwise chain_l, packed M)", 11
+        else:
+            flops = P * 4.0 * N * N * 128
+            kname, kdesc, n_launch = "attention_h3_kernel<4>", "attention_h3_kernel<4,xcd>", 12
+        achieved = flops / (att_ms * 1e-3) / 1e12
+        att_prof = profiled(kname, grid)
+        roofline = {"kernel": kdesc, "bound": "mfma",
                     "achieved": round(achieved, 3), "peak": round(PEAK_H3_TFLOPS, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_H3_TFLOPS, 4),
                     "traffic": att_prof and att_prof["hbm_bytes"],
                     "traffic_unit": "HBM bytes per launch (rocprofv3 2*FETCH_SIZE+WRITE_SIZE)",
                     "profile": att_prof,
-                    "peak_note": "fp16 MFMA 2500 TFLOP/s / 3 products per fp32 product; "
-                                 "exact-fp32 MFMA peak is 157.3",
+                    "peak_note": "fp16 MFMA 2500 TFLOP/s / 3 products per fp32 product (the attention's; "
+                                 "the fused chain's convolutions take 4); exact-fp32 MFMA peak is 157.3",
                     "fp16_mfma_util": round(3 * achieved / PEAK_F16_MFMA_TFLOPS, 4),
                     "launch_ms": round(att_ms, 4), "launches_timed": len(att_times),
-                    "flop_per_launch": flops, "share_of_step": round(12 * att_ms / ms_per_step, 3)}
+                    "flop_per_launch": flops, "share_of_step": round(n_launch * att_ms / ms_per_step, 3)}
         sp = ctypes.c_void_p(stream.cuda_stream)
         Mo = torch.empty((P, N, N), dtype=torch.float32, device=dev)
         sd = model.sigma_spat.detach()

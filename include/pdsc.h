@@ -131,6 +131,13 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
  * live in the encoder workspace).                                           */
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *Npad, int32_t *nsplit);
 
+/* The encoder's launch plan for (B, N, precision) (no reference counterpart):
+ * *fused = 1 when every layer but the last runs its attention and the
+ * following pointwise chain (fc_message, residual, PointCN, Q/K/V) as ONE
+ * launch -- these are then the launches pdsc_attention_timing times -- and 0
+ * when attention and chain are separate launches.                           */
+int32_t pdsc_encoder_plan(int32_t B, int32_t N, int32_t precision, int32_t *fused);
+
 /* Measurement hook (bench.py): while capacity > 0, every attention launch the
  * encoder issues from the calling thread records start_events[i] / stop_events[i]
  * (hipEvent_t) around itself on its stream, i = (*count)++ while < capacity.

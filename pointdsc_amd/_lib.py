@@ -63,6 +63,7 @@ _PROTOS = {
     "pdsc_attention_f32": (c_int32, [vp, vp, vp, vp, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),
     "pdsc_attention_layout": (c_int32, [c_int32, c_int32, c_int32, ctypes.POINTER(c_int32),
                                         ctypes.POINTER(c_int32)]),
+    "pdsc_encoder_plan": (c_int32, [c_int32, c_int32, c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_attention_timing": (c_int32, [ctypes.POINTER(vp), ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_forward_timing": (c_int32, [ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),

@@ -82,7 +82,8 @@ int check_cfg(const pdsc_config *cfg) {
 
 struct Dims {
     int B, N, Npad, S, k, T, nsplit;
-    bool f32;  // PDSC_PRECISION_F32
+    bool f32;   // PDSC_PRECISION_F32
+    bool fuse;  // attention + pointwise chain in one launch per layer (attention_fused)
 };
 
 int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
@@ -96,14 +97,16 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     d.T = cfg->num_iterations;
     d.f32 = cfg->precision == PDSC_PRECISION_F32;
     d.nsplit = attention_nsplit(B, N, d.f32);
+    d.fuse = attention_fused(B, N, d.f32);
     if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
     if (d.k > 63) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 63", d.k);
     return PDSC_OK;
 }
 
 struct EncBufs {
-    float *feat, *opart, *ml, *vexp;
-    _Float16 *q, *k, *v;  // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
+    float *feat, *opart, *ml, *vexp, *vexp2;
+    _Float16 *q, *k, *v;     // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
+    _Float16 *q2, *k2, *v2;  // the other Q/K/V set of the fused path (layers alternate), else null
 };
 
 EncBufs carve_encoder(Carve &c, const Dims &d) {
@@ -116,6 +119,14 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
     e.opart = c.take<float>(rows * d.nsplit);
     e.ml = c.take<float>((size_t)d.B * d.Npad * d.nsplit * 2);
     e.vexp = c.take<float>((size_t)d.B * (d.Npad / 32));
+    e.q2 = e.k2 = e.v2 = nullptr;
+    e.vexp2 = nullptr;
+    if (d.fuse) {
+        e.q2 = c.take<_Float16>(2 * rows);
+        e.k2 = c.take<_Float16>(2 * rows);
+        e.v2 = c.take<_Float16>(2 * rows);
+        e.vexp2 = c.take<float>((size_t)d.B * (d.Npad / 32));
+    }
     return e;
 }
 
@@ -123,6 +134,25 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                 bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s) {
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s));
+    if (d.fuse) {  // layers 0 .. L-2 fused, Q/K/V alternating between the two sets; the last one split
+        _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
+        float *vx = e.vexp, *vx2 = e.vexp2;
+        for (int l = 0; l + 1 < lay.L; ++l) {
+            const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
+            if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
+            HIPCHK(launch_attn_pw2(packed, lay, l, q, k, v, vx, M, m_packed, d.B, d.N, d.Npad, e.feat, q2, k2, v2, vx2,
+                                   s));
+            if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
+            std::swap(q, q2);
+            std::swap(k, k2);
+            std::swap(v, v2);
+            std::swap(vx, vx2);
+        }
+        HIPCHK(launch_attention(q, k, v, vx, M, m_packed, false, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
+        HIPCHK(launch_pw_last(packed, lay, false, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, feat_out, normed,
+                              normed_s, conf, s));
+        return PDSC_OK;
+    }
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
@@ -417,6 +447,12 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
     *nsplit = attention_nsplit(B, N, precision == PDSC_PRECISION_F32);
+    return PDSC_OK;
+}
+
+int32_t pdsc_encoder_plan(int32_t B, int32_t N, int32_t precision, int32_t *fused) {
+    if (B < 1 || N < 1 || !fused) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    *fused = attention_fused(B, N, precision == PDSC_PRECISION_F32) ? 1 : 0;
     return PDSC_OK;
 }
 

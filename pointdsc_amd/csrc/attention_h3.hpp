@@ -201,30 +201,37 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
     return g;
 }
 
-// PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
-// vexp: [B][Npad/32] V-tile exponents (see above).
-template <int NW, bool XCD, bool PACKED>
-__global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
-    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
-    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
-    float *__restrict__ ml) {
-    extern __shared__ __attribute__((aligned(16))) char h3smem[];
-    // block -> (pair, query block, split), a pair's blocks kept on one XCD
+// Workgroup -> (pair, query block, split), a pair's blocks kept on one XCD
+// (consecutive workgroup ids round-robin over the 8 XCDs).
+struct AttnBlock {
+    int b, qb, split;
+};
+PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
     const int G = g.B * g.nqb * g.nsplit;
     int lid = blockIdx.x;
-    if (XCD) {
+    if (xcd) {
         const int full = G & ~7;
         if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
     }
-    const int split = lid % g.nsplit;
-    const int qb = (lid / g.nsplit) % g.nqb;
-    const int b = lid / g.nsplit / g.nqb;
+    return AttnBlock{lid / g.nsplit / g.nqb, (lid / g.nsplit) % g.nqb, lid % g.nsplit};
+}
 
+// The attention of one workgroup (NW waves x 32 queries of pair b, query block
+// qb, key-tile split `split`): every wave runs the tile loop (the barriers)
+// and, for queries < Npad, leaves this lane's un-normalised O^T (lane <-> query,
+// tile t register r <-> channel 32t + acc_row(r, h)), the running max m (log2
+// units, + PSHIFT) and the full row sum l (both lane halves).  smem: the K/V
+// ring (attention_h3_lds_bytes), free again when this returns.
+// PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
+// vexp: [B][Npad/32] V-tile exponents (see above).
+template <int NW, bool PACKED>
+PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks,
+                                const _Float16 *__restrict__ Vs, const float *__restrict__ vexp,
+                                const float *__restrict__ M, const AttnGridH3 &g, const AttnBlock &blk, char *h3smem,
+                                int wave, int lane, f32x16 (&O)[4], float &m_run, float &l_run) {
+    const int b = blk.b, qb = blk.qb, split = blk.split;
     const int N = g.N, Npad = g.Npad;
-    // wave in an SGPR: every wave-uniform branch below (M orientation, active,
-    // the barrier's count) is then a scalar branch, never an exec-masked one
-    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5,
-              l32 = lane & 31;
+    const int h = lane >> 5, l32 = lane & 31;
     const int q0 = qb * (NW * 32) + wave * 32;
     const int nst = (N + H3_TILE - 1) / H3_TILE;
     const int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
@@ -262,8 +269,10 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
         }
     };
 
-    f32x16 O[4] = {zero16(), zero16(), zero16(), zero16()};
-    float m_run = -INFINITY, l_run = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) O[t] = zero16();
+    m_run = -INFINITY;
+    l_run = 0.0f;
     const float scale = 0.12751743082459868f;  // log2(e) / sqrt(128)
     const uint32_t Nb = (uint32_t)N * 4;
 
@@ -410,9 +419,25 @@ __global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
         }
         sync();
     }
-    if (!active) return;
-
     l_run += __shfl_xor(l_run, 32);
+}
+
+template <int NW, bool XCD, bool PACKED>
+__global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
+    float *__restrict__ ml) {
+    extern __shared__ __attribute__((aligned(16))) char h3smem[];
+    const AttnBlock blk = attention_h3_block(g, XCD);
+    const int b = blk.b, split = blk.split, Npad = g.Npad;
+    // wave in an SGPR: every wave-uniform branch (M orientation, active, the
+    // barrier's count) is then a scalar branch, never an exec-masked one
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5;
+    const int q0 = blk.qb * (NW * 32) + wave * 32, qq = q0 + (lane & 31);
+    f32x16 O[4];
+    float m_run, l_run;
+    attention_h3_core<NW, PACKED>(Qs, Ks, Vs, vexp, M, g, blk, h3smem, wave, lane, O, m_run, l_run);
+    if (q0 >= Npad) return;
     const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
     // registers 8u + 4g .. +3 of tile t = fragment block 2 (2t + u) + g (16 coalesced 1-KiB stores)
     float *Ob = opart + obase * CH + (size_t)(q0 >> 5) * (H3_TILE * CH) + 4 * lane;

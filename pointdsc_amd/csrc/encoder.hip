@@ -1046,6 +1046,38 @@ PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const W2Sched 
     if (active) w2_store_v(acc, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * H3_TILE_H, vexp + (row >> 5), lane);
 }
 
+// Coefficients of combine + fc_message + PointCN + QKV (pw2_mid / attn_pw2).
+struct W2CoefMid {
+    static constexpr int f0 = W2CoefQKV::end, f3 = f0 + 3 * CH2, f6 = f3 + 3 * CH2, end = f6 + 3 * CH;
+};
+static_assert(W2CoefMid::end <= PW2_COEF, "coefficient table");
+PDSC_DEV void w2_coef_mid(float *cf, const float *__restrict__ pk, const PwMsg &m, const PwDense4 &d, int tid) {
+    w2_coef_qkv(cf, pk, d, tid);
+    w2_coef(cf + W2CoefMid::f0, pk, m.fc0, CH2, tid);
+    w2_coef(cf + W2CoefMid::f3, pk, m.fc3, CH2, tid);
+    w2_coef(cf + W2CoefMid::f6, pk, m.fc6, CH, tid);
+}
+
+// fc_message + residual + PointCN + QKV from the message fragments x (after the
+// combine); the pipeline is at fc0's first chunk.  featL, Q, K, V, vexp: the pair's.
+PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sched &S, const float *cf, const PwMsg &m,
+                           const PwDense4 &d, f16x8 *xh, f16x8 *xl, float *__restrict__ featL,
+                           _Float16 *__restrict__ Q, _Float16 *__restrict__ K, _Float16 *__restrict__ V,
+                           float *__restrict__ vexp, int row, bool active, int wave, int lane) {
+    f32x16 a2[2], a4[4], res[4];
+    f16x8 yh[8], yl[8];
+    w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
+    if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + W2CoefMid::f0, nullptr, yh, yl, lane);
+    w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
+    if (active) {
+        w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + W2CoefMid::f3, nullptr, xh, xl, lane);
+        w2_load_row(featL, row, lane, res);  // the residual: lands during fc6's MFMAs
+    }
+    w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
+    if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + W2CoefMid::f6, res, yh, yl, lane);
+    w2_pcn_qkv(P, pk, S, cf, d, yh, yl, featL, Q, K, V, vexp, row, active, wave, lane);
+}
+
 #define PW2_PROLOGUE                                                                              \
     extern __shared__ __attribute__((aligned(16))) char w2smem[];                                 \
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5; \
@@ -1104,28 +1136,59 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const 
                                                                _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                                _Float16 *__restrict__ V, float *__restrict__ vexp) {
     PW2_PROLOGUE
-    constexpr int CF0 = W2CoefQKV::end, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2;
-    static_assert(CF6 + 3 * CH <= PW2_COEF, "coefficient table");
-    w2_coef_qkv(cf, pk, d, tid);
-    w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
-    w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
-    w2_coef(cf + CF6, pk, m.fc6, CH, tid);
+    w2_coef_mid(cf, pk, m, d, tid);
     f16x8 xh[8], xl[8];
     if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
     __syncthreads();
-    f32x16 a2[2], a4[4], res[4];
-    f16x8 yh[8], yl[8];
-    w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
-    if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + CF0, nullptr, yh, yl, lane);
-    w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
-    if (active) {
-        w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
-        w2_load_row(featL + boff, row, lane, res);  // the residual: lands during fc6's MFMAs
+    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                 vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+}
+
+// attention_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1} in ONE
+// launch (one key split: the workgroup's 128 queries are the 128 points of its
+// chain): the O^T accumulators the attention core leaves in registers are the
+// message's k-step fragments, so the partials never touch HBM, and workgroups
+// in their attention phase overlap others' store-heavy chain phase.  Reads the
+// layer-l Q/K/V (Qs, Ks, Vs, vexp_in) and writes the layer-(l+1) ones to other
+// buffers (Q, K, V, vexp): other workgroups of the pair still read layer l.
+// Bit-identical to attention_h3_kernel + pw2_mid_kernel (a one-split combine
+// is O * (1 / l) exactly).  LDS: the K/V ring, then the weight ring.
+template <bool PACKED>
+__global__ __launch_bounds__(PW2_W * 64, 2) void attn_pw2_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp_in, const float *__restrict__ M, AttnGridH3 g, const float *__restrict__ pk,
+    W2Sched S, PwMsg m, PwDense4 d, float *__restrict__ featL, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+    _Float16 *__restrict__ V, float *__restrict__ vexp) {
+    extern __shared__ __attribute__((aligned(16))) char w2smem[];
+    const AttnBlock blk = attention_h3_block(g, true);
+    const int b = blk.b, Npad = g.Npad, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
+              lane = tid & 63;
+    const int row = blk.qb * PW2_PTS + wave * 32 + (lane & 31);
+    const bool active = blk.qb * PW2_PTS + wave * 32 < Npad;  // wave-uniform
+    const size_t boff = (size_t)b * Npad * CH;
+    f32x16 O[4];
+    float m_run, l_run;
+    attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
+    // the K/V ring is free (the core ends on a barrier): weight chunks 0, 1 and the coefficients
+    W2Pipe P{w2smem, 0};
+    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);
+    w2_stage(pk, S, 0, P.slot(0), wave, lane);
+    w2_stage(pk, S, 1, P.slot(1), wave, lane);
+    w2_coef_mid(cf, pk, m, d, tid);
+    f16x8 xh[8], xl[8];
+    if (active) {  // msg = O / l: registers 8u .. 8u+7 of tile t = k-step 2t + u
+        const float rl = 1.0f / l_run;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = O[ks >> 1][8 * (ks & 1) + e] * rl;
+            split8v(v, xh[ks], xl[ks]);
+        }
     }
-    w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
-    if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + CF6, res, yh, yl, lane);
-    w2_pcn_qkv(P, pk, S, cf, d, yh, yl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-               vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+    __syncthreads();
+    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                 vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
 }
 
 // combine + fc_message + residual, then F.normalize (:156) and the classifier (:171).
@@ -1243,6 +1306,36 @@ static W2Sched sched_msg(const PwMsg &m) {
 
 static PwDense4 dense4(const LayerOff &l) { return PwDense4{l.pcn, l.q, l.k, l.v}; }
 static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
+
+// attn_pw2 wherever pw2 runs and the attention has one key split (knob
+// PDSC_FUSE=0 keeps the two launches; measurement only).
+bool attention_fused(int B, int N, bool f32) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_FUSE");
+        return e && e[0] == '0';
+    }();
+    const int Npad = round_up(N, QB);
+    return !off && use_pw2(B, Npad, f32) && prod_grid(B, N).nsplit == 1;
+}
+
+hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
+                           const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
+                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s) {
+    const AttnGridH3 g = prod_grid(B, N);
+    if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
+    const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
+    const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
+    const _Float16 *qs = static_cast<const _Float16 *>(q), *ks = static_cast<const _Float16 *>(k),
+                   *vs = static_cast<const _Float16 *>(v);
+    _Float16 *Q = static_cast<_Float16 *>(qo), *K = static_cast<_Float16 *>(ko), *V = static_cast<_Float16 *>(vo);
+    if (m_packed)
+        hipLaunchKernelGGL(attn_pw2_kernel<true>, dim3(g.B * g.nqb), dim3(PW2_W * 64), lds, s, qs, ks, vs, vexp_in, M,
+                           g, packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), feat, Q, K, V, vexp_out);
+    else
+        hipLaunchKernelGGL(attn_pw2_kernel<false>, dim3(g.B * g.nqb), dim3(PW2_W * 64), lds, s, qs, ks, vs, vexp_in, M,
+                           g, packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), feat, Q, K, V, vexp_out);
+    return hipGetLastError();
+}
 
 // Point-tile size: 64 points (two 32-row MFMA tiles per wave, 2 workgroups per
 // CU) once the launch has >= 2 workgroups per CU, else 32 (twice the

@@ -143,6 +143,13 @@ int attention_nsplit(int B, int N, bool f32);
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s);
+// attention_l fused with pw_mid_l (encoder.hip: attn_pw2_kernel) for this shape?
+bool attention_fused(int B, int N, bool f32);
+// attention of layer `layer` on (q, k, v, vexp_in) + the pointwise chain to the
+// layer-(layer+1) (qo, ko, vo, vexp_out), H3 layouts; feat updated in place.
+hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
+                           const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
+                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s);
 // fp32 rows [B][N][CH] -> [B][Npad][CH], padding rows zero.
 hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).

@@ -244,6 +244,52 @@ def test_batched_equals_single(B, gpu_device):
         np.testing.assert_allclose(r["final_trans"][0].cpu().numpy(), T[i].cpu().numpy(), atol=2 * POSE_ATOL)
 
 
+def _fusion_outputs(dev, B=64, N=1000):
+    """Encoder (dense M) and forward (packed M) outputs at a shape the encoder
+    plan fuses (attention + pointwise chain per launch)."""
+    from pointdsc_amd import kernels
+    from pointdsc_amd.synthetic import synthetic_batch
+    g = load_golden("rel_1k")
+    m = _model(g, dev)
+    cfg, packed = m.pdsc_config(), m.packed_weights()
+    b = synthetic_batch(B, N, seed=21)
+    corr, src, tgt = (_t(b[k], dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    M = kernels.compat(src, tgt, torch.tensor([float(g["sigma_d"])], device=dev))
+    feat, normed, conf = kernels.encoder(cfg, packed, corr, M)
+    T, L, fconf, seeds = kernels.forward_testing(cfg, packed, corr, src, tgt, debug=True)
+    return {k: v.cpu().numpy() for k, v in dict(feat=feat, normed=normed, conf=conf, T=T, L=L, fconf=fconf,
+                                                  seeds=seeds).items()}
+
+
+def _dump_fusion_outputs(path):  # child process entry (PDSC_FUSE=0)
+    np.savez(path, **_fusion_outputs(torch.device("cuda:0")))
+
+
+def test_fused_encoder_bit_identical(gpu_device, tmp_path):
+    """attn_pw2_kernel (attention_l + the pointwise chain_l in one launch, partials
+    kept in registers) gives exactly the bits of the separate attention_h3 +
+    pw2_mid launches (run in a child process with the PDSC_FUSE=0 knob): encoder
+    features / confidences with dense M, and the whole forward with packed M."""
+    import ctypes
+    import os
+    import subprocess
+    import sys
+    from pointdsc_amd import _lib
+    fused = ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(64, 1000, 0, ctypes.byref(fused)), "encoder_plan")
+    assert fused.value == 1
+    ours = _fusion_outputs(gpu_device)
+    out = tmp_path / "unfused.npz"
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PDSC_FUSE="0")
+    code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+           f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r})"
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+    ref = np.load(out)
+    for k, v in ours.items():
+        assert np.array_equal(v, ref[k]), k
+
+
 def test_graph_replay_equals_eager(gpu_device):
     """ForwardPlan.capture(): a HIP-graph replay of the forward gives the eager
     result bitwise, and picks up new contents of the same input buffers; the
