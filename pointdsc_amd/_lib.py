@@ -11,7 +11,10 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpdsc.so")
+# PDSC_LIB_VARIANT=<v> loads libpdsc_<v>.so (an A/B build of the same sources,
+# `make -C pointdsc_amd/csrc variant V=<v> VFLAGS=...`; measurement only)
+_VARIANT = os.environ.get("PDSC_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, f"libpdsc_{_VARIANT}.so" if _VARIANT else "libpdsc.so")
 
 c_int32, c_size_t, c_float, c_double = ctypes.c_int32, ctypes.c_size_t, ctypes.c_float, ctypes.c_double
 vp = ctypes.c_void_p

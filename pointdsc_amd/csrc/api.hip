@@ -134,7 +134,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                 bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s) {
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s));
-    if (d.fuse) {  // layers 0 .. L-2 fused, Q/K/V alternating between the two sets; the last one split
+    if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
         float *vx = e.vexp, *vx2 = e.vexp2;
         for (int l = 0; l + 1 < lay.L; ++l) {
@@ -148,9 +148,8 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
             std::swap(v, v2);
             std::swap(vx, vx2);
         }
-        HIPCHK(launch_attention(q, k, v, vx, M, m_packed, false, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml, s));
-        HIPCHK(launch_pw_last(packed, lay, false, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, feat_out, normed,
-                              normed_s, conf, s));
+        HIPCHK(launch_attn_pw2_last(packed, lay, q, k, v, vx, M, m_packed, d.B, d.N, d.Npad, e.feat, feat_out, normed,
+                                    normed_s, conf, s));
         return PDSC_OK;
     }
     for (int l = 0; l < lay.L; ++l) {

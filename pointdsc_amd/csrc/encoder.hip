@@ -738,7 +738,11 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 // epilogue coefficients (bias, BN alpha / beta) sit in LDS for the launch.
 // Two workgroups per CU (~55 KiB of LDS and <= 256 VGPRs each) overlap one's
 // HBM phases and epilogues with the other's MFMAs.
-constexpr int PW2_W = 4;                              // waves per workgroup: 128 points
+#ifndef PW2_WAVES
+#define PW2_WAVES 4
+#endif
+constexpr int PW2_W = PW2_WAVES;                      // waves per workgroup (32 points each)
+constexpr int PW2_OCC = PW2_W >= 8 ? 1 : 2;           // workgroups per CU (<= 256 VGPRs: 2 waves per SIMD)
 constexpr int PW2_CB = 8;                             // blocks per chunk (24 KiB)
 constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 planes)
 constexpr int PW2_SLOT = PW2_CB * PW2_BLKB;
@@ -746,9 +750,6 @@ constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
 constexpr size_t PW2_LDS = 2 * PW2_SLOT + PW2_COEF * sizeof(float);
 constexpr int W2_MAXCH = 24;
-#ifndef PW2_MID_OCC
-#define PW2_MID_OCC 2
-#endif
 
 struct W2Sched {                 // chunk c: np[c] pieces of 1 KiB starting at pk-halfs off[c]
     uint32_t off[W2_MAXCH];
@@ -930,6 +931,19 @@ PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restric
     }
 }
 
+// The O^T accumulators of the attention core -> the message's k-step fragments
+// (msg = O / l; registers 8u .. 8u+7 of tile t = k-step 2t + u).
+PDSC_DEV void w2_msg_frags(const f32x16 (&O)[4], float l_run, f16x8 *xh, f16x8 *xl) {
+    const float rl = 1.0f / l_run;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = O[ks >> 1][8 * (ks & 1) + e] * rl;
+        split8v(v, xh[ks], xl[ks]);
+    }
+}
+
 // This lane's 64 fp32 values of a 128-channel row.  featL keeps the lane-register
 // order of a transposed 128-output layer in the fragment-block tiling of the
 // attention partials (per 32-row tile, block 4t + q = registers 4q .. 4q+3 of
@@ -1091,7 +1105,7 @@ PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sche
 
 // layer0 (Conv1d in_dim -> 128 on exact fp32 MFMA 32x32x2, k-step j: inputs 2j + h)
 // + PointCN_0 + QKV_0.
-__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *__restrict__ pk, W2Sched S, size_t l0w,
+__global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_first_kernel(const float *__restrict__ pk, W2Sched S, size_t l0w,
                                                                  size_t l0b, PwDense4 d, const float *__restrict__ corr,
                                                                  int in_dim, int N, int Npad, float *__restrict__ featL,
                                                                  _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
@@ -1129,7 +1143,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_first_kernel(const float *_
 }
 
 // combine_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1}.
-__global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
+__global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
                                                                PwDense4 d, const float *__restrict__ opart,
                                                                const float *__restrict__ ml, int nsplit, int N,
                                                                int Npad, float *__restrict__ featL,
@@ -1154,7 +1168,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_MID_OCC) void pw2_mid_kernel(const 
 // Bit-identical to attention_h3_kernel + pw2_mid_kernel (a one-split combine
 // is O * (1 / l) exactly).  LDS: the K/V ring, then the weight ring.
 template <bool PACKED>
-__global__ __launch_bounds__(PW2_W * 64, 2) void attn_pw2_kernel(
+__global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp_in, const float *__restrict__ M, AttnGridH3 g, const float *__restrict__ pk,
     W2Sched S, PwMsg m, PwDense4 d, float *__restrict__ featL, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
@@ -1176,40 +1190,38 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void attn_pw2_kernel(
     w2_stage(pk, S, 1, P.slot(1), wave, lane);
     w2_coef_mid(cf, pk, m, d, tid);
     f16x8 xh[8], xl[8];
-    if (active) {  // msg = O / l: registers 8u .. 8u+7 of tile t = k-step 2t + u
-        const float rl = 1.0f / l_run;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = O[ks >> 1][8 * (ks & 1) + e] * rl;
-            split8v(v, xh[ks], xl[ks]);
-        }
-    }
+    if (active) w2_msg_frags(O, l_run, xh, xl);  // msg = O / l
     __syncthreads();
     w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
 }
 
-// combine + fc_message + residual, then F.normalize (:156) and the classifier (:171).
-__global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
-    const float *__restrict__ pk, W2Sched S, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
-    const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
-    const float *__restrict__ featL, float *__restrict__ feat_out, float *__restrict__ normed,
-    _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
-    PW2_PROLOGUE
-    constexpr int CF0 = 0, CF3 = CF0 + 3 * CH2, CF6 = CF3 + 3 * CH2, CC0 = CF6 + 3 * CH, CC2 = CC0 + 3 * CLS,
-                  CC4 = CC2 + 3 * CLS;
-    static_assert(CC4 + CLS <= PW2_COEF, "coefficient table");
-    w2_coef(cf + CF0, pk, m.fc0, CH2, tid);
-    w2_coef(cf + CF3, pk, m.fc3, CH2, tid);
-    w2_coef(cf + CF6, pk, m.fc6, CH, tid);
-    w2_coef(cf + CC0, pk, c0, CLS, tid);
-    w2_coef(cf + CC2, pk, c2, CLS, tid);
-    for (int i = tid; i < CLS; i += PW2_W * 64) cf[CC4 + i] = pk[c4w + i];
-    f16x8 xh[8], xl[8];
-    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
-    __syncthreads();
+// Coefficients of the last layer's fc_message + classifier (pw2_last / attn_pw2_last).
+struct W2CoefLast {
+    static constexpr int f0 = 0, f3 = f0 + 3 * CH2, f6 = f3 + 3 * CH2, c0 = f6 + 3 * CH, c2 = c0 + 3 * CLS,
+                         c4 = c2 + 3 * CLS, end = c4 + CLS;
+};
+static_assert(W2CoefLast::end <= PW2_COEF, "coefficient table");
+PDSC_DEV void w2_coef_last(float *cf, const float *__restrict__ pk, const PwMsg &m, const DenseOff &c0,
+                           const DenseOff &c2, size_t c4w, int tid) {
+    w2_coef(cf + W2CoefLast::f0, pk, m.fc0, CH2, tid);
+    w2_coef(cf + W2CoefLast::f3, pk, m.fc3, CH2, tid);
+    w2_coef(cf + W2CoefLast::f6, pk, m.fc6, CH, tid);
+    w2_coef(cf + W2CoefLast::c0, pk, c0, CLS, tid);
+    w2_coef(cf + W2CoefLast::c2, pk, c2, CLS, tid);
+    for (int i = tid; i < CLS; i += PW2_W * 64) cf[W2CoefLast::c4 + i] = pk[c4w + i];
+}
+
+// fc_message + residual from the message fragments x, then F.normalize (:156)
+// and the classifier (:171); the pipeline is at fc0's first chunk.  featL: the pair's.
+PDSC_DEV void w2_last_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sched &S, const float *cf, const PwMsg &m,
+                            const DenseOff &c0, const DenseOff &c2, size_t c4b, f16x8 *xh, f16x8 *xl,
+                            const float *__restrict__ featL, float *__restrict__ feat_out, float *__restrict__ normed,
+                            _Float16 *__restrict__ normed_s, float *__restrict__ conf, int b, int N, int row,
+                            bool active, int wave, int lane) {
+    constexpr int CF0 = W2CoefLast::f0, CF3 = W2CoefLast::f3, CF6 = W2CoefLast::f6, CC0 = W2CoefLast::c0,
+                  CC2 = W2CoefLast::c2, CC4 = W2CoefLast::c4;
+    const int h = lane >> 5;
     f32x16 a1[1], a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];
     w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
@@ -1217,7 +1229,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
     w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + CF3, nullptr, xh, xl, lane);
-        w2_load_row(featL + boff, row, lane, res);
+        w2_load_row(featL, row, lane, res);
     }
     w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     const bool in = row < N;
@@ -1228,7 +1240,7 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
         for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) ss = __builtin_fmaf(a4[t][r], a4[t][r], ss);
-        ss += __shfl_xor(ss, 32);
+        ss = halves_sum(ss);
         const float den = fmaxf(sqrtf(ss), 1e-12f);
         if (in) {
             float *dst = normed + ((size_t)b * N + row) * CH;
@@ -1272,9 +1284,55 @@ __global__ __launch_bounds__(PW2_W * 64, 2) void pw2_last_kernel(
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int e = 0; e < 8; ++e) s = __builtin_fmaf(cf[CC4 + w2_chan(0, u, e, h)], a1[0][8 * u + e], s);
-        s += __shfl_xor(s, 32);
+        s = halves_sum(s);
         if (in && h == 0) conf[(size_t)b * N + row] = s + pk[c4b];
     }
+}
+
+// combine + fc_message + residual, then F.normalize (:156) and the classifier (:171).
+__global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_last_kernel(
+    const float *__restrict__ pk, W2Sched S, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b,
+    const float *__restrict__ opart, const float *__restrict__ ml, int nsplit, int N, int Npad,
+    const float *__restrict__ featL, float *__restrict__ feat_out, float *__restrict__ normed,
+    _Float16 *__restrict__ normed_s, float *__restrict__ conf) {
+    PW2_PROLOGUE
+    w2_coef_last(cf, pk, m, c0, c2, c4w, tid);
+    f16x8 xh[8], xl[8];
+    if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
+    __syncthreads();
+    w2_last_chain(P, pk, S, cf, m, c0, c2, c4b, xh, xl, featL + boff, feat_out, normed, normed_s, conf, b, N, row,
+                  active, wave, lane);
+}
+
+// attention_{L-1} + fc_message_{L-1} + residual + normalize + classifier in ONE
+// launch (as attn_pw2_kernel for the last layer): bit-identical to
+// attention_h3_kernel + pw2_last_kernel with one key split.
+template <bool PACKED>
+__global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_last_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp_in, const float *__restrict__ M, AttnGridH3 g, const float *__restrict__ pk,
+    W2Sched S, PwMsg m, DenseOff c0, DenseOff c2, size_t c4w, size_t c4b, const float *__restrict__ featL,
+    float *__restrict__ feat_out, float *__restrict__ normed, _Float16 *__restrict__ normed_s,
+    float *__restrict__ conf) {
+    extern __shared__ __attribute__((aligned(16))) char w2smem[];
+    const AttnBlock blk = attention_h3_block(g, true);
+    const int b = blk.b, N = g.N, Npad = g.Npad, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
+              lane = tid & 63;
+    const int row = blk.qb * PW2_PTS + wave * 32 + (lane & 31);
+    const bool active = blk.qb * PW2_PTS + wave * 32 < Npad;  // wave-uniform
+    f32x16 O[4];
+    float m_run, l_run;
+    attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
+    W2Pipe P{w2smem, 0};
+    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);
+    w2_stage(pk, S, 0, P.slot(0), wave, lane);
+    w2_stage(pk, S, 1, P.slot(1), wave, lane);
+    w2_coef_last(cf, pk, m, c0, c2, c4w, tid);
+    f16x8 xh[8], xl[8];
+    if (active) w2_msg_frags(O, l_run, xh, xl);
+    __syncthreads();
+    w2_last_chain(P, pk, S, cf, m, c0, c2, c4b, xh, xl, featL + (size_t)b * Npad * CH, feat_out, normed, normed_s,
+                  conf, b, N, row, active, wave, lane);
 }
 #undef PW2_PROLOGUE
 
@@ -1286,7 +1344,7 @@ static bool use_pw2(int B, int Npad, bool f32) {
         return e ? atoi(e) : 1;
     }();
     if (f32 || mode == 0) return false;
-    return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) >= 512;
+    return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) * PW2_W >= 2048;  // >= 2 waves per SIMD
 }
 
 static W2Sched sched_qkv(W2Sched S, const PwDense4 &d) {
@@ -1309,19 +1367,21 @@ static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
 // attn_pw2 wherever pw2 runs and the attention has one key split (knob
 // PDSC_FUSE=0 keeps the two launches; measurement only).
+static AttnGridH3 fused_grid(int B, int N) { return attention_h3_grid<PW2_W>(B, N, att_target()); }
 bool attention_fused(int B, int N, bool f32) {
     static const bool off = [] {
         const char *e = getenv("PDSC_FUSE");
         return e && e[0] == '0';
     }();
     const int Npad = round_up(N, QB);
-    return !off && use_pw2(B, Npad, f32) && prod_grid(B, N).nsplit == 1;
+    const AttnGridH3 g = fused_grid(B, N);
+    return !off && use_pw2(B, Npad, f32) && g.nsplit == 1 && g.nqb * PW2_PTS == Npad;
 }
 
 hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
                            const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
                            float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s) {
-    const AttnGridH3 g = prod_grid(B, N);
+    const AttnGridH3 g = fused_grid(B, N);
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
     const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
     const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
@@ -1334,6 +1394,30 @@ hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer
     else
         hipLaunchKernelGGL(attn_pw2_kernel<false>, dim3(g.B * g.nqb), dim3(PW2_W * 64), lds, s, qs, ks, vs, vexp_in, M,
                            g, packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), feat, Q, K, V, vexp_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, const void *q, const void *k,
+                                const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N,
+                                int Npad, const float *feat, float *feat_out, float *normed, _Float16 *normed_s,
+                                float *conf, hipStream_t s) {
+    const AttnGridH3 g = fused_grid(B, N);
+    if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad) return hipErrorInvalidValue;
+    W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
+    w2_sched_add(S, lay.c0, CH, CLS);
+    w2_sched_add(S, lay.c2, CLS, CLS);
+    const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
+    const _Float16 *qs = static_cast<const _Float16 *>(q), *ks = static_cast<const _Float16 *>(k),
+                   *vs = static_cast<const _Float16 *>(v);
+    const PwMsg m = msg3(lay.layer[lay.L - 1]);
+    if (m_packed)
+        hipLaunchKernelGGL(attn_pw2_last_kernel<true>, dim3(g.B * g.nqb), dim3(PW2_W * 64), lds, s, qs, ks, vs, vexp_in,
+                           M, g, packed, S, m, lay.c0, lay.c2, lay.c4_w, lay.c4_b, feat, feat_out, normed, normed_s,
+                           conf);
+    else
+        hipLaunchKernelGGL(attn_pw2_last_kernel<false>, dim3(g.B * g.nqb), dim3(PW2_W * 64), lds, s, qs, ks, vs,
+                           vexp_in, M, g, packed, S, m, lay.c0, lay.c2, lay.c4_w, lay.c4_b, feat, feat_out, normed,
+                           normed_s, conf);
     return hipGetLastError();
 }
 

@@ -463,10 +463,13 @@ constexpr int KMAX = 64;
 // Power iteration of one seed's k x k matrix (models/PointDSC.py:347-358), one
 // wave: lane a holds row a of T in registers, v is broadcast from LDS 4 entries
 // at a time.  hist[t][a] = iterate t+1; returns bit t = allclose(v_{t+1}, v_t).
+// KC: k rounded up to a multiple of 16 (columns past k are zero, their FMAs
+// exact no-ops), so k = 40 runs 48-long rows instead of KMAX = 64.
+template <int KC>
 PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T, float *vbuf, float *hb, int a) {
-    float trow[KMAX];
+    float trow[KC];
 #pragma unroll
-    for (int c = 0; c < KMAX; ++c) trow[c] = (a < k && c < k) ? trow_lds[a * tstride + c] : 0.0f;
+    for (int c = 0; c < KC; ++c) trow[c] = (a < k && c < k) ? trow_lds[a * tstride + c] : 0.0f;
     vbuf[a] = 1.0f;
     float v = (a < k) ? 1.0f : 0.0f;
     unsigned flags = 0;
@@ -474,7 +477,7 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
     for (int t = 0; t < T; ++t) {
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int c = 0; c < KMAX; c += 4) {
+        for (int c = 0; c < KC; c += 4) {
             const f32x4 vv = *reinterpret_cast<const f32x4 *>(&vbuf[c]);
             acc[0] = __builtin_fmaf(trow[c], vv[0], acc[0]);
             acc[1] = __builtin_fmaf(trow[c + 1], vv[1], acc[1]);
@@ -508,7 +511,7 @@ constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
 
 // F32 (PDSC_PRECISION_F32): the Gram tiles on exact fp32 MFMA from the fp32
 // normed rows (`feats` = normed [B][N][128]); H3: `feats` = the split copy.
-template <bool F32>
+template <bool F32, int KC>
 __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict__ feats,
                                                        const float *__restrict__ src,
                                                        const float *__restrict__ tgt,
@@ -575,44 +578,56 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
             }
         }
     }
-    __builtin_amdgcn_wave_barrier();  // P visible to the wave
-    // T for one 32 x 32 Gram tile: rows 32 ta + acc_row(r, h), columns 32 tb + l32
-    auto emit = [&](const f32x16 &G, int ta, int tb) {
+    // The Gram tiles' strict upper triangle (a < c < k) to LDS, then T = F o S
+    // evaluated once per unordered pair with the pairs dealt evenly over the
+    // 64 lanes (triangular index p -> (a, c)): ceil(k(k-1)/128) passes instead
+    // of 16 per Gram tile with most lanes masked off.  Each pair is read and
+    // overwritten in place by the one lane that owns it, then mirrored.
+    auto gstore = [&](const f32x16 &G, int ta, int tb) {
         const int c = 32 * tb + l32;
-        const f32x4 pc0 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR);
-        const f32x4 pc1 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR + 4);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int a = 32 * ta + acc_row(r, h);
-            if (a >= k || c >= k || (ta == tb && a > c)) continue;  // each unordered pair once
-            float val = 0.0f;
-            if (a != c) {
-                const f32x4 pa0 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR);
-                const f32x4 pa1 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR + 4);
-                // correctly rounded '/' and sqrtf through their fma-corrected forms
-                // (pdsc_common.hpp; exact for normal operands, within 1 ulp below 2^-96)
-                const float fm = fmaxf(1.0f - cr_div(1.0f - G[r], sig2, rsig2), 0.0f);  // :259
-                float dx = pa0[0] - pc0[0], dy = pa0[1] - pc0[1], dz = pa0[2] - pc0[2];
-                const float ds = cr_sqrt((dx * dx + dy * dy) + dz * dz);    // :268
-                dx = pa0[3] - pc0[3];
-                dy = pa1[0] - pc1[0];
-                dz = pa1[1] - pc1[1];
-                const float dt = cr_sqrt((dx * dx + dy * dy) + dz * dz);
-                const float dd = ds - dt;
-                const float sm = fmaxf(1.0f - cr_div(dd * dd, sd2, rsd2), 0.0f);     // :270
-                val = fm * sm;                                            // :277 (diag 0, :278)
-            }
-            Tl[a * tls + c] = val;
-            Tl[c * tls + a] = val;
+            if (a < c && c < k) Tl[a * tls + c] = G[r];
         }
     };
-    emit(G00, 0, 0);
+    gstore(G00, 0, 0);
     if (nt > 1) {
-        emit(G01, 0, 1);
-        emit(G11, 1, 1);
+        gstore(G01, 0, 1);
+        gstore(G11, 1, 1);
+    }
+    if (lane < k) Tl[lane * tls + lane] = 0.0f;  // diag 0 (:278)
+    __builtin_amdgcn_wave_barrier();  // P and the Gram triangle visible to the wave
+    const int npair = k * (k - 1) / 2, k2 = 2 * k - 1;
+    for (int p = lane; p < npair; p += 64) {
+        // row a: pairs before it S(a) = a (2k - 1 - a) / 2 <= p < S(a + 1)
+        int a = (int)(0.5f * ((float)k2 - sqrtf((float)(k2 * k2 - 8 * p))));
+        a = max(0, min(a, k - 2));
+        if ((a + 1) * (k2 - a - 1) / 2 <= p) ++a;
+        if (a * (k2 - a) / 2 > p) --a;
+        const int c = p - a * (k2 - a) / 2 + a + 1;
+        const float g = Tl[a * tls + c];
+        const f32x4 pa0 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR);
+        const f32x4 pa1 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR + 4);
+        const f32x4 pc0 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR);
+        const f32x4 pc1 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR + 4);
+        // correctly rounded '/' and sqrtf through their fma-corrected forms
+        // (pdsc_common.hpp; exact for normal operands, within 1 ulp below 2^-96)
+        const float fm = fmaxf(1.0f - cr_div(1.0f - g, sig2, rsig2), 0.0f);  // :259
+        float dx = pa0[0] - pc0[0], dy = pa0[1] - pc0[1], dz = pa0[2] - pc0[2];
+        const float ds = cr_sqrt((dx * dx + dy * dy) + dz * dz);    // :268
+        dx = pa0[3] - pc0[3];
+        dy = pa1[0] - pc1[0];
+        dz = pa1[1] - pc1[1];
+        const float dt = cr_sqrt((dx * dx + dy * dy) + dz * dz);
+        const float dd = ds - dt;
+        const float sm = fmaxf(1.0f - cr_div(dd * dd, sd2, rsd2), 0.0f);     // :270
+        const float val = fm * sm;                                            // :277
+        Tl[a * tls + c] = val;
+        Tl[c * tls + a] = val;
     }
     __builtin_amdgcn_wave_barrier();
-    const unsigned flags = power_iterate(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
+    const unsigned flags = power_iterate<KC>(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
     if (lane == 0) atomicAnd(&pair_mask[b], flags);
 }
 
@@ -627,12 +642,18 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const size_t lds = nsm_seed_lds_bytes(k, wpb);
-    if (f32)
-        hipLaunchKernelGGL(nsm_seed_kernel<true>, grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma,
-                           sigma_d, hist, pair_mask);
-    else
-        hipLaunchKernelGGL(nsm_seed_kernel<false>, grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma,
-                           sigma_d, hist, pair_mask);
+#define NSM_LAUNCH(F, KC)                                                                                     \
+    hipLaunchKernelGGL((nsm_seed_kernel<F, KC>), grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma, \
+                       sigma_d, hist, pair_mask)
+    const int kc = (k + 15) / 16;
+    if (f32) {
+        if (kc == 1) NSM_LAUNCH(true, 16); else if (kc == 2) NSM_LAUNCH(true, 32);
+        else if (kc == 3) NSM_LAUNCH(true, 48); else NSM_LAUNCH(true, 64);
+    } else {
+        if (kc == 1) NSM_LAUNCH(false, 16); else if (kc == 2) NSM_LAUNCH(false, 32);
+        else if (kc == 3) NSM_LAUNCH(false, 48); else NSM_LAUNCH(false, 64);
+    }
+#undef NSM_LAUNCH
     return hipGetLastError();
 }
 

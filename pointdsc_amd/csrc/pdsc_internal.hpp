@@ -150,6 +150,12 @@ bool attention_fused(int B, int N, bool f32);
 hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
                            const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
                            float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s);
+// attention of the last layer on (q, k, v, vexp_in) + its fc_message, residual,
+// F.normalize and classifier (encoder.hip: attn_pw2_last_kernel); outputs as launch_pw_last.
+hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, const void *q, const void *k,
+                                const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N,
+                                int Npad, const float *feat, float *feat_out, float *normed, _Float16 *normed_s,
+                                float *conf, hipStream_t s);
 // fp32 rows [B][N][CH] -> [B][Npad][CH], padding rows zero.
 hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
