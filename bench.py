@@ -253,7 +253,10 @@ def main():
         log(f"[rank {rank}] --gpus {args.gpus} but WORLD_SIZE={world}: the process group decides (n_gpus={world})")
     if args.launcher_selftest:
         return selftest(args, world, rank)
-    if world > 1:
+    # a process group whenever a launcher started this rank (torchrun or our own
+    # spawn set RANK), so even a 1-rank job runs its gather / max-reduce on RCCL
+    grp = world > 1 or "RANK" in os.environ
+    if grp:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://")
@@ -291,7 +294,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     def barrier():
-        if world > 1:
+        if grp:
             torch.distributed.barrier()
 
     # HIP events around every attention launch inside the timed region (the
@@ -314,7 +317,7 @@ def main():
     L.pdsc_attention_timing(None, None, 0, None)
     L.pdsc_forward_timing(None, 0, None)
     att_times = [evs.elapsed_ms(i) for i in range(evs.count.value)]
-    if world > 1:
+    if grp:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -524,7 +527,7 @@ def main():
             "stages_ms": stages, "single_pair": single, "exact_f32": exact, "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if grp:
         torch.distributed.destroy_process_group()
 
 

@@ -187,6 +187,11 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
     return mfma_h(wh, xh, c);
 }
 
+#ifdef ATT_DIAG_NODMA
+#define ATT_DIAG_DMA_PIECES 0
+#else
+#define ATT_DIAG_DMA_PIECES (32 / NW)
+#endif
 template <int NW>
 constexpr size_t attention_h3_lds_bytes() { return (size_t)2 * (H3_KTB + H3_VTB); }
 
@@ -373,12 +378,15 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // pieces (issued after them) may be outstanding.  Dense: the compiler's own
     // waits apply.
     auto wait_m = [&](float (&mv)[16], float &ev) {
+#if defined(ATT_DIAG_NOM)
+        return;
+#endif
         if constexpr (PACKED)
             asm volatile("s_waitcnt vmcnt(%17)"
                          : "+v"(mv[0]), "+v"(mv[1]), "+v"(mv[2]), "+v"(mv[3]), "+v"(mv[4]), "+v"(mv[5]), "+v"(mv[6]),
                            "+v"(mv[7]), "+v"(mv[8]), "+v"(mv[9]), "+v"(mv[10]), "+v"(mv[11]), "+v"(mv[12]),
                            "+v"(mv[13]), "+v"(mv[14]), "+v"(mv[15]), "+v"(ev)
-                         : "n"(32 / NW));
+                         : "n"(ATT_DIAG_DMA_PIECES));
     };
 
     // One key tile: M loads first (they land while QK^T runs), K and V fragments
@@ -487,11 +495,20 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         // (issued by padding waves too -- their reads stay inside the pair's M
         // -- so every path reaches the softmax with the same count outstanding)
         float mv[16], ev;
+#ifdef ATT_DIAG_NOM  // diagnostic build (wrong results): no M / exponent loads
+        for (int r = 0; r < 16; ++r) mv[r] = 1.0f;
+        ev = 0.0f;
+#else
         load_m(st * H3_TILE, mv, ev);
+#endif
         __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the DMA
         // unconditional (the last tile re-copies itself into the idle slot) so
         // the vmcnt the softmax waits with is the same on every path
+#ifndef ATT_DIAG_NODMA  // diagnostic build (wrong results): only tile st0 is ever copied
         stage(min(st + 1, st1 - 1), slot ^ 1);
+#else
+        if (st == st0) stage(st0, slot ^ 1);
+#endif
         {  // padding waves (q0 >= Npad) compute on clamped operands and store nothing
             const char *base = h3smem + slot * (H3_KTB + H3_VTB);
             tile(base, base + H3_KTB, st * H3_TILE, mv, ev);

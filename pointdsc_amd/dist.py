@@ -43,7 +43,7 @@ def gather_rows(rows, n_items, device=None):
     rows = torch.as_tensor(rows)
     if rows.dim() != 2 or rows.shape[0] != shard_count(n_items, rank, W):
         raise ValueError(f"rank {rank}: rows {tuple(rows.shape)} but owns {shard_count(n_items, rank, W)} pairs")
-    if W == 1:
+    if not (dist.is_available() and dist.is_initialized()):  # no process group: nothing to gather
         return rows.clone()
     dev = device if device is not None else rows.device
     per = shard_count(n_items, 0, W)  # rank 0 owns the most
@@ -63,7 +63,7 @@ def job_throughput(units, seconds, device=None):
     """(total units over all ranks, max seconds over ranks): the whole-job
     rate is their ratio (the slowest rank bounds the job)."""
     rank, W = world()
-    if W == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(units), float(seconds)
     dev = device if device is not None else torch.device("cpu")
     u = torch.tensor([float(units)], dtype=torch.float64, device=dev)

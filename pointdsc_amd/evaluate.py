@@ -160,7 +160,8 @@ def evaluate_synthetic(model, n_pairs, num_corr, preset="3dmatch", batch=16, see
         extra = torch.tensor([[t_model, t_data, 0.0]], dtype=torch.float64).expand(len(idx), 3)
         rows.append(torch.cat([st, extra], dim=1))
     mine_rows = torch.cat(rows) if rows else torch.zeros((0, 12), dtype=torch.float64)
-    gdev = device if (W > 1 and device is not None and device.type == "cuda") else None
+    grp = torch.distributed.is_available() and torch.distributed.is_initialized()
+    gdev = device if (grp and device is not None and device.type == "cuda") else None
     allrows = dist.gather_rows(mine_rows, n_pairs, device=gdev).cpu().numpy()
     return allrows, aggregate(allrows)
 
@@ -187,7 +188,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if W > 1:
+    grp = W > 1 or "RANK" in os.environ  # launched by torchrun: RCCL even for one rank
+    if grp:
         tdist.init_process_group("nccl", init_method="env://")
     p = PRESETS[a.preset]
     m = PointDSC(num_layers=12, inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"],
@@ -199,7 +201,7 @@ def main():
     if not tdist.is_initialized() or tdist.get_rank() == 0:
         save_outputs(stats, a.log, a.save_npy)
         print(json.dumps(summary))
-    if W > 1:
+    if grp:
         tdist.destroy_process_group()
 
 
