@@ -187,11 +187,6 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
     return mfma_h(wh, xh, c);
 }
 
-#ifdef ATT_DIAG_NODMA
-#define ATT_DIAG_DMA_PIECES 0
-#else
-#define ATT_DIAG_DMA_PIECES (32 / NW)
-#endif
 template <int NW>
 constexpr size_t attention_h3_lds_bytes() { return (size_t)2 * (H3_KTB + H3_VTB); }
 
@@ -378,15 +373,12 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // pieces (issued after them) may be outstanding.  Dense: the compiler's own
     // waits apply.
     auto wait_m = [&](float (&mv)[16], float &ev) {
-#if defined(ATT_DIAG_NOM)
-        return;
-#endif
         if constexpr (PACKED)
             asm volatile("s_waitcnt vmcnt(%17)"
                          : "+v"(mv[0]), "+v"(mv[1]), "+v"(mv[2]), "+v"(mv[3]), "+v"(mv[4]), "+v"(mv[5]), "+v"(mv[6]),
                            "+v"(mv[7]), "+v"(mv[8]), "+v"(mv[9]), "+v"(mv[10]), "+v"(mv[11]), "+v"(mv[12]),
                            "+v"(mv[13]), "+v"(mv[14]), "+v"(mv[15]), "+v"(ev)
-                         : "n"(ATT_DIAG_DMA_PIECES));
+                         : "n"(32 / NW));
     };
 
     // One key tile: M loads first (they land while QK^T runs), K and V fragments
@@ -486,34 +478,39 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // priority 1 for the whole loop (MI355X_MICROARCH.md, two waves per SIMD, item 4)
     if (NW >= 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
+    // M (and the V exponent) of tile t are loaded at the END of tile t - 1,
+    // after its PV MFMAs and before the barrier: they land during the barrier
+    // and the next QK^T (measured: the M loads cost 15 % of the launch when
+    // issued at the tile start; the same launch with no M traffic at all).
+    // The barrier then waits only for the DMA (issued before those loads):
+    // vmcnt(number of M loads of the next tile), a scalar-branch immediate.
+    auto sync_m = [&](int key0) {
+        if constexpr (PACKED) {
+            if (key0 / MPACK_T <= q0 / MPACK_T)
+                __builtin_amdgcn_s_waitcnt(0x4071);  // vmcnt(17) lgkmcnt(0): 16 M rows + the exponent
+            else
+                __builtin_amdgcn_s_waitcnt(0x0075);  // vmcnt(5) lgkmcnt(0): 4 M quads + the exponent
+            __builtin_amdgcn_s_barrier();
+        } else {
+            sync();
+        }
+    };
+    float mv[16], ev;
     if (st0 < st1) stage(st0, 0);
-    sync();
+    load_m(st0 * H3_TILE, mv, ev);
+    sync_m(st0 * H3_TILE);
     for (int st = st0; st < st1; ++st) {
         const int slot = (st - st0) & 1;
-        // this tile's M and V exponent BEFORE the next tile's DMA: the softmax
-        // then waits for them with vmcnt(DMA pieces), not for the DMA as well
-        // (issued by padding waves too -- their reads stay inside the pair's M
-        // -- so every path reaches the softmax with the same count outstanding)
-        float mv[16], ev;
-#ifdef ATT_DIAG_NOM  // diagnostic build (wrong results): no M / exponent loads
-        for (int r = 0; r < 16; ++r) mv[r] = 1.0f;
-        ev = 0.0f;
-#else
-        load_m(st * H3_TILE, mv, ev);
-#endif
-        __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the DMA
         // unconditional (the last tile re-copies itself into the idle slot) so
         // the vmcnt the softmax waits with is the same on every path
-#ifndef ATT_DIAG_NODMA  // diagnostic build (wrong results): only tile st0 is ever copied
         stage(min(st + 1, st1 - 1), slot ^ 1);
-#else
-        if (st == st0) stage(st0, slot ^ 1);
-#endif
         {  // padding waves (q0 >= Npad) compute on clamped operands and store nothing
             const char *base = h3smem + slot * (H3_KTB + H3_VTB);
             tile(base, base + H3_KTB, st * H3_TILE, mv, ev);
         }
-        sync();
+        const int nx = min(st + 1, st1 - 1) * H3_TILE;
+        load_m(nx, mv, ev);  // (padding waves' reads stay inside the pair's M)
+        sync_m(nx);
     }
 #ifdef ATT_PRIO_HALF
     __builtin_amdgcn_s_setprio(0);
