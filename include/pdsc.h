@@ -167,7 +167,10 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
  * (ascending distance, ascending index) is dropped positionally.
  * Replaces models/common.py:48-69 + models/PointDSC.py:250-252 (only the
  * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k];
- * 1 <= k <= 63, k + 1 <= N.  precision: enum pdsc_precision (distances).   */
+ * 1 <= k <= 63, k + 1 <= N.  precision: enum pdsc_precision (distances).
+ * The workspace holds the [B,S,N] distance rows (H3 opt-in PDSC_KNN_FUSED=1:
+ * one fused launch that writes them only for seeds whose tie group overflows
+ * its candidate lists).                                                      */
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S);
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
                       int32_t S, int32_t k, int32_t precision, int32_t *knn, void *workspace,

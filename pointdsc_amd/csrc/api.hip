@@ -467,8 +467,37 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
 }
 
 // -------------------------------------------------------------------- a6
+// H3 seed kNN: knn_dist + knn_select (default), or knn_fused_kernel with the knob
+// PDSC_KNN_FUSED=1 (bit-identical; measured 1.9x / 2.2x SLOWER at N = 1000 / 5000:
+// each wave ranks 8 seeds' candidates serially and sweeps its key tiles with a
+// one-tile register prefetch, both latency-bound -- DESIGN.md section 7)
+static bool knn_fused_on() {
+    static const bool on = [] {
+        const char *e = getenv("PDSC_KNN_FUSED");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+// a6 (:250-252) for the forwards: knn [B][S][k]; dist [B][S][N] and redo [B][S] scratch
+int run_seed_knn(const float *normed, const _Float16 *normed_s, bool f32, const int *seeds, int B, int N, int S,
+                 int k, float *dist, int *redo, int *knn, hipStream_t s) {
+    HIPCHK(hipMemsetAsync(knn, 0, sizeof(int) * B * S * k, s));
+    if (f32) {
+        HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s));
+    } else if (knn_fused_on()) {
+        HIPCHK(launch_seed_knn_fused(normed_s, seeds, B, N, S, k, dist, knn, redo, s));
+        return PDSC_OK;
+    } else {
+        HIPCHK(launch_knn_dist(normed_s, seeds, B, N, S, dist, s));
+    }
+    HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
+    return PDSC_OK;
+}
+
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S) {
-    return align_bytes((size_t)B * S * N * sizeof(float)) + align_bytes((size_t)B * N * 2 * CH * sizeof(_Float16));
+    return align_bytes((size_t)B * S * N * sizeof(float)) + align_bytes((size_t)B * N * 2 * CH * sizeof(_Float16)) +
+           align_bytes((size_t)B * S * sizeof(int));
 }
 
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
@@ -484,14 +513,10 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
     Carve c(ws);
     float *dist = c.take<float>((size_t)B * S * N);
     _Float16 *ns = c.take<_Float16>((size_t)B * N * 2 * CH);
-    if (precision == PDSC_PRECISION_F32) {
-        HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s));
-    } else {
-        HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
-        HIPCHK(launch_knn_dist(ns, seeds, B, N, S, dist, s));
-    }
-    HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
-    return PDSC_OK;
+    int *redo = c.take<int>((size_t)B * S);
+    const bool f32 = precision == PDSC_PRECISION_F32;
+    if (!f32) HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
+    return run_seed_knn(normed, ns, f32, seeds, B, N, S, k, dist, redo, knn, s);
 }
 
 // ----------------------------------------------------------------- a7-a8
@@ -608,12 +633,8 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
     STAGE(3);
     // a6 (:250-252)
-    HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
-    if (d.f32)
-        HIPCHK(launch_knn_dist_f32(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
-    else
-        HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
-    HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
+    // (f.counts: the hypotheses' inlier counts later, the overflow flags here)
+    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
     STAGE(4);
     // a7-a8 (:257-282)
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
@@ -670,12 +691,8 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(f.lm), 0x3f800000u, (size_t)d.B * d.N, s));
     HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
     // a6-a10 as in testing (:182 -> cal_seed_trans), no post-refinement (:185-186)
-    HIPCHK(hipMemsetAsync(f.knn, 0, sizeof(int) * d.B * d.S * d.k, s));
-    if (d.f32)
-        HIPCHK(launch_knn_dist_f32(f.normed, f.seeds, d.B, d.N, d.S, f.kdist, s));
-    else
-        HIPCHK(launch_knn_dist(f.normed_s, f.seeds, d.B, d.N, d.S, f.kdist, s));
-    HIPCHK(launch_knn_select(f.kdist, d.B, d.N, d.S, d.k, f.knn, s));
+    // (f.counts: the hypotheses' inlier counts later, the overflow flags here)
+    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm,
                    f.weights, nullptr, s));
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold, f.seed_trans,
