@@ -194,13 +194,6 @@ PDSC_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
 }
 
-// The same buffer descriptor as an SGPR quad for inline asm ("s" operand).
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-PDSC_DEV i32x4 h3_rsrc_s(const void *base, uint32_t bytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(base);
-    return i32x4{(int)(uint32_t)a, (int)(uint32_t)(a >> 32), (int)bytes, 0x00020000};
-}
-
 struct AttnGridH3 {
     int B, N, Npad, nqb, nsplit, sps;  // sps = 32-key tiles per split
 };
@@ -297,8 +290,6 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
 
     const float *vexp_b = vexp + (size_t)b * (Npad / H3_TILE);
     const __amdgpu_buffer_rsrc_t rE = h3_rsrc(vexp_b, (uint32_t)(Npad / H3_TILE) * 4u);
-    const i32x4 rsM = h3_rsrc_s(M + (size_t)b * mper, (uint32_t)(mper * 4u));
-    const i32x4 rsE = h3_rsrc_s(vexp_b, (uint32_t)(Npad / H3_TILE) * 4u);
     // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys of tile key0
     auto load_m = [&](int key0, float (&mv)[16], float &ev) {
         if constexpr (PACKED) {
@@ -310,54 +301,22 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             static_assert(MPACK_T == 32, "one packed tile per wave step");
             const int kt = key0 / MPACK_T, qt = q0 / MPACK_T;
             const int kr = 4 * h, qr = l32;
-            // Inline asm, with the tile's V exponent as a 17th / 5th load: the
-            // compiler does not count LDS-DMA in vmcnt and would wait for
-            // vmcnt(0) -- the next tile's DMA too -- before the softmax; the
-            // tile waits with an explicit vmcnt(DMA pieces) instead (h3_wait_m).
-            const uint32_t eo = (uint32_t)(key0 / H3_TILE) * 4u;
             if (kt <= qt) {  // rows = keys
                 const uint32_t vo =
                     ((uint32_t)mpack_tile(kt, qt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(kr * MPACK_T + qr)) * 4;
-                asm volatile(
-                    "buffer_load_dword %0, %17, %18, 0 offen\n\t"
-                    "buffer_load_dword %1, %17, %18, 0 offen offset:128\n\t"
-                    "buffer_load_dword %2, %17, %18, 0 offen offset:256\n\t"
-                    "buffer_load_dword %3, %17, %18, 0 offen offset:384\n\t"
-                    "buffer_load_dword %4, %17, %18, 0 offen offset:1024\n\t"
-                    "buffer_load_dword %5, %17, %18, 0 offen offset:1152\n\t"
-                    "buffer_load_dword %6, %17, %18, 0 offen offset:1280\n\t"
-                    "buffer_load_dword %7, %17, %18, 0 offen offset:1408\n\t"
-                    "buffer_load_dword %8, %17, %18, 0 offen offset:2048\n\t"
-                    "buffer_load_dword %9, %17, %18, 0 offen offset:2176\n\t"
-                    "buffer_load_dword %10, %17, %18, 0 offen offset:2304\n\t"
-                    "buffer_load_dword %11, %17, %18, 0 offen offset:2432\n\t"
-                    "buffer_load_dword %12, %17, %18, 0 offen offset:3072\n\t"
-                    "buffer_load_dword %13, %17, %18, 0 offen offset:3200\n\t"
-                    "buffer_load_dword %14, %17, %18, 0 offen offset:3328\n\t"
-                    "buffer_load_dword %15, %17, %18, 0 offen offset:3456\n\t"
-                    "buffer_load_dword %16, %19, %20, 0 offen"
-                    : "=&v"(mv[0]), "=&v"(mv[1]), "=&v"(mv[2]), "=&v"(mv[3]), "=&v"(mv[4]), "=&v"(mv[5]),
-                      "=&v"(mv[6]), "=&v"(mv[7]), "=&v"(mv[8]), "=&v"(mv[9]), "=&v"(mv[10]), "=&v"(mv[11]),
-                      "=&v"(mv[12]), "=&v"(mv[13]), "=&v"(mv[14]), "=&v"(mv[15]), "=&v"(ev)
-                    : "v"(vo), "s"(rsM), "v"(eo), "s"(rsE));
-                return;
-            }
-            {  // rows = queries
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    mv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                          rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * (MPACK_T * 4), 0, 0));
+            } else {  // rows = queries
                 const uint32_t vo =
                     ((uint32_t)mpack_tile(qt, kt, mnt) * (MPACK_T * MPACK_T) + (uint32_t)(qr * MPACK_T + kr)) * 4;
-                f32x4 v4[4];
-                asm volatile(
-                    "buffer_load_dwordx4 %0, %5, %6, 0 offen\n\t"
-                    "buffer_load_dwordx4 %1, %5, %6, 0 offen offset:32\n\t"
-                    "buffer_load_dwordx4 %2, %5, %6, 0 offen offset:64\n\t"
-                    "buffer_load_dwordx4 %3, %5, %6, 0 offen offset:96\n\t"
-                    "buffer_load_dword %4, %7, %8, 0 offen"
-                    : "=&v"(v4[0]), "=&v"(v4[1]), "=&v"(v4[2]), "=&v"(v4[3]), "=&v"(ev)
-                    : "v"(vo), "s"(rsM), "v"(eo), "s"(rsE));
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM, vo + 32 * g, 0, 0));
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[g][e];
+                    for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[e];
+                }
             }
         } else {
             const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
@@ -365,22 +324,11 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             for (int r = 0; r < 16; ++r)
                 mv[r] = __builtin_bit_cast(
                     float, __builtin_amdgcn_raw_buffer_load_b32(rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb, 0, 0));
-            ev = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, (uint32_t)(key0 / H3_TILE) * 4u, 0, 0));
         }
+        // the tile's V exponent as a vector load with the M loads (a scalar load
+        // here was waited for with lgkmcnt(0) in the middle of the softmax)
+        ev = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, (uint32_t)(key0 / H3_TILE) * 4u, 0, 0));
     };
-    // Before the first use of this tile's M / V exponent: PACKED, the asm loads
-    // are invisible to the compiler -- wait until only the next tile's DMA
-    // pieces (issued after them) may be outstanding.  Dense: the compiler's own
-    // waits apply.
-    auto wait_m = [&](float (&mv)[16], float &ev) {
-        if constexpr (PACKED)
-            asm volatile("s_waitcnt vmcnt(%17)"
-                         : "+v"(mv[0]), "+v"(mv[1]), "+v"(mv[2]), "+v"(mv[3]), "+v"(mv[4]), "+v"(mv[5]), "+v"(mv[6]),
-                           "+v"(mv[7]), "+v"(mv[8]), "+v"(mv[9]), "+v"(mv[10]), "+v"(mv[11]), "+v"(mv[12]),
-                           "+v"(mv[13]), "+v"(mv[14]), "+v"(mv[15]), "+v"(ev)
-                         : "n"(32 / NW));
-    };
-
     // One key tile: M loads first (they land while QK^T runs), K and V fragments
     // read two blocks ahead of their MFMAs (three register sets; sched_barrier
     // keeps the compiler from sinking each read onto its MFMA).  (Prefetching M
@@ -404,7 +352,6 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             S = mfma_h3(kf[j % 3][0], kf[j % 3][1], qh[j], ql[j], S);
             __builtin_amdgcn_sched_barrier(0);
         }
-        wait_m(mv, ev);
         float p[16];
         float mx = -INFINITY;
 #pragma unroll
@@ -473,48 +420,24 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         __builtin_amdgcn_s_barrier();
     };
 
-#ifdef ATT_PRIO_HALF
-    // A/B knob (measurement only): the second half of an 8-wave workgroup at
-    // priority 1 for the whole loop (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if (NW >= 8 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-    // M (and the V exponent) of tile t are loaded at the END of tile t - 1,
-    // after its PV MFMAs and before the barrier: they land during the barrier
-    // and the next QK^T (measured: the M loads cost 15 % of the launch when
-    // issued at the tile start; the same launch with no M traffic at all).
-    // The barrier then waits only for the DMA (issued before those loads):
-    // vmcnt(number of M loads of the next tile), a scalar-branch immediate.
-    auto sync_m = [&](int key0) {
-        if constexpr (PACKED) {
-            if (key0 / MPACK_T <= q0 / MPACK_T)
-                __builtin_amdgcn_s_waitcnt(0x4071);  // vmcnt(17) lgkmcnt(0): 16 M rows + the exponent
-            else
-                __builtin_amdgcn_s_waitcnt(0x0075);  // vmcnt(5) lgkmcnt(0): 4 M quads + the exponent
-            __builtin_amdgcn_s_barrier();
-        } else {
-            sync();
-        }
-    };
-    float mv[16], ev;
+    // (Measured and reverted: M and the exponent loaded by inline asm with an
+    // explicit vmcnt -- the compiler waits vmcnt(0), the next tile's DMA
+    // included, because it does not count LDS-DMA -- issued at the tile start
+    // or at the end of the previous tile: no faster, and the compiler copies
+    // asm-loaded registers before the wait.  DESIGN.md section 7.)
     if (st0 < st1) stage(st0, 0);
-    load_m(st0 * H3_TILE, mv, ev);
-    sync_m(st0 * H3_TILE);
+    sync();
     for (int st = st0; st < st1; ++st) {
         const int slot = (st - st0) & 1;
-        // unconditional (the last tile re-copies itself into the idle slot) so
-        // the vmcnt the softmax waits with is the same on every path
-        stage(min(st + 1, st1 - 1), slot ^ 1);
+        float mv[16], ev;
+        load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
+        if (st + 1 < st1) stage(st + 1, slot ^ 1);
         {  // padding waves (q0 >= Npad) compute on clamped operands and store nothing
             const char *base = h3smem + slot * (H3_KTB + H3_VTB);
             tile(base, base + H3_KTB, st * H3_TILE, mv, ev);
         }
-        const int nx = min(st + 1, st1 - 1) * H3_TILE;
-        load_m(nx, mv, ev);  // (padding waves' reads stay inside the pair's M)
-        sync_m(nx);
+        sync();
     }
-#ifdef ATT_PRIO_HALF
-    __builtin_amdgcn_s_setprio(0);
-#endif
     l_run = halves_sum(l_run);
 }
 
