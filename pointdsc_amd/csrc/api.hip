@@ -178,7 +178,7 @@ NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
     NsmBufs n;
     n.ns = own_split ? c.take<_Float16>((size_t)B * N * 2 * CH) : nullptr;
     n.hist = c.take<float>((size_t)B * S * std::max(T, 1) * k);
-    n.mask = c.take<unsigned>((size_t)B);
+    n.mask = c.take<unsigned>((size_t)B * S);  // per-seed allclose bits
     n.weights = c.take<float>((size_t)B * S * k);
     return n;
 }
@@ -188,7 +188,6 @@ NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
 int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float *src, const float *tgt,
             const int *knn, int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d,
             const NsmBufs &nb, float *weights, int *iters, hipStream_t s) {
-    HIPCHK(hipMemsetAsync(nb.mask, 0xff, sizeof(unsigned) * B, s));
     if (!f32 && !normed_s) {
         HIPCHK(launch_split_rows(normed, (size_t)B * N, nb.ns, s));
         normed_s = nb.ns;

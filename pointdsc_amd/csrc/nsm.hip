@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
                                                        const int *__restrict__ knn, int N, int S, int k, int T,
                                                        const float *__restrict__ sigma_p,
                                                        const float *__restrict__ sigma_d_p,
-                                                       float *__restrict__ hist, unsigned *__restrict__ pair_mask) {
+                                                       float *__restrict__ hist, unsigned *__restrict__ seed_flags) {
     extern __shared__ __attribute__((aligned(16))) float nsm_sdyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.y, s = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -827,7 +827,9 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     }
     __builtin_amdgcn_wave_barrier();
     const unsigned flags = power_iterate<KC>(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
-    if (lane == 0) atomicAnd(&pair_mask[b], flags);
+    // this seed's allclose bits; nsm_finish ANDs a pair's seeds (a per-pair
+    // atomicAnd here serialised S atomics per address: 30-60 us of the launch)
+    if (lane == 0) seed_flags[(size_t)b * S + s] = flags;
 }
 
 size_t nsm_seed_lds_bytes(int k, int wpb) {
@@ -836,14 +838,14 @@ size_t nsm_seed_lds_bytes(int k, int wpb) {
 
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
                            int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
-                           unsigned *pair_mask, hipStream_t s) {
+                           unsigned *seed_flags, hipStream_t s) {
     if (k < 1 || k > KMAX) return hipErrorInvalidValue;
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const size_t lds = nsm_seed_lds_bytes(k, wpb);
 #define NSM_LAUNCH(F, KC)                                                                                     \
     hipLaunchKernelGGL((nsm_seed_kernel<F, KC>), grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma, \
-                       sigma_d, hist, pair_mask)
+                       sigma_d, hist, seed_flags)
     const int kc = (k + 15) / 16;
     if (f32) {
         if (kc == 1) NSM_LAUNCH(true, 16); else if (kc == 2) NSM_LAUNCH(true, 32);
@@ -858,11 +860,18 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
 
 // w = v_{t*} / (sum v_{t*} + 1e-6)  (models/PointDSC.py:280-282)
 __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict__ hist,
-                                                        const unsigned *__restrict__ pair_mask, int S,
+                                                        const unsigned *__restrict__ seed_flags, int S,
                                                         int k, int T, float *__restrict__ weights,
                                                         int *__restrict__ iters_used) {
     const int b = blockIdx.y, s = blockIdx.x, a = threadIdx.x;
-    const unsigned m = pair_mask[b] & ((T >= 32) ? 0xffffffffu : ((1u << T) - 1u));
+    // the pair-global allclose bits: AND over the pair's S seeds (torch.allclose
+    // over the pair's [S, k] iterate, :354)
+    unsigned all = 0xffffffffu;
+    if (T > 0)
+        for (int q = a; q < S; q += 64) all &= seed_flags[(size_t)b * S + q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) all &= (unsigned)__shfl_xor((int)all, o);
+    const unsigned m = all & ((T >= 32) ? 0xffffffffu : ((1u << T) - 1u));
     const int tstar = m ? (__ffs(m)) : T;  // 1-based iterate index
     float v = 1.0f;
     if (tstar > 0 && a < k) v = hist[(((size_t)b * S + s) * T + (tstar - 1)) * k + a];
@@ -872,9 +881,9 @@ __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict_
     if (s == 0 && a == 0 && iters_used) iters_used[b] = tstar;
 }
 
-hipError_t launch_nsm_finish(const float *hist, const unsigned *pair_mask, int B, int S, int k, int T,
+hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T,
                              float *weights, int *iters_used, hipStream_t s) {
-    hipLaunchKernelGGL(nsm_finish_kernel, dim3(S, B), dim3(64), 0, s, hist, pair_mask, S, k, T,
+    hipLaunchKernelGGL(nsm_finish_kernel, dim3(S, B), dim3(64), 0, s, hist, seed_flags, S, k, T,
                        weights, iters_used);
     return hipGetLastError();
 }
