@@ -748,7 +748,10 @@ constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 plan
 constexpr int PW2_SLOT = PW2_CB * PW2_BLKB;
 constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
-constexpr size_t PW2_LDS = 2 * PW2_SLOT + PW2_COEF * sizeof(float);
+#ifndef PW2_NSLOT
+#define PW2_NSLOT 2  // weight-ring slots (A/B build knob: 3 = two chunks in flight)
+#endif
+constexpr size_t PW2_LDS = PW2_NSLOT * PW2_SLOT + PW2_COEF * sizeof(float);
 constexpr int W2_MAXCH = 24;
 
 struct W2Sched {                 // chunk c: np[c] pieces of 1 KiB starting at pk-halfs off[c]
@@ -784,7 +787,7 @@ PDSC_DEV void w2_stage(const float *pk, const W2Sched &S, int c, char *slot, int
 struct W2Pipe {
     char *base;
     int c;  // chunk being multiplied
-    PDSC_DEV char *slot(int k) const { return base + (k & 1) * PW2_SLOT; }
+    PDSC_DEV char *slot(int k) const { return base + (k % PW2_NSLOT) * PW2_SLOT; }
 };
 
 // End of a chunk: this wave's DMA of the next chunk has landed (all but its
@@ -796,6 +799,25 @@ PDSC_DEV void w2_sync(bool active) {
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
     else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// w2_sync with a run-time count (wave-uniform): the 3-slot ring waits for chunk
+// c + 1 while chunk c + 2's pieces (and the caller's younger stores) stay in flight.
+#define W2_SYNC_CASE(n) \
+    case n: asm volatile("s_waitcnt vmcnt(" #n ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+PDSC_DEV void w2_sync_n(int n, bool active) {
+    n = __builtin_amdgcn_readfirstlane(active ? n : 0);
+    switch (n) {
+        W2_SYNC_CASE(1) W2_SYNC_CASE(2) W2_SYNC_CASE(3) W2_SYNC_CASE(4) W2_SYNC_CASE(5) W2_SYNC_CASE(6)
+        W2_SYNC_CASE(7) W2_SYNC_CASE(16) W2_SYNC_CASE(17) W2_SYNC_CASE(18) W2_SYNC_CASE(19) W2_SYNC_CASE(20)
+        W2_SYNC_CASE(21) W2_SYNC_CASE(22) W2_SYNC_CASE(23)
+        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
+#undef W2_SYNC_CASE
+// this wave's LDS-DMA pieces of chunk c (w2_stage's loop count)
+PDSC_DEV int w2_pieces(const W2Sched &S, int c, int wave) {
+    return (c < S.n && S.np[c] > wave) ? (S.np[c] - wave + PW2_W - 1) / PW2_W : 0;
 }
 
 PDSC_DEV void w2_frag(const char *bp, f16x8 (&w)[3]) {
@@ -838,11 +860,15 @@ PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const W2Sched &S, const f16x8
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (active) w2_mma<NKS, NT, TRANS>(P.slot(P.c), xh, xl, acc, c * NT, lane);
-        if (c == 0)
-            w2_sync<NST>(active);
-        else
-            w2_sync<0>(active);
-        w2_stage(pk, S, P.c + 2, P.slot(P.c), wave, lane);
+        if constexpr (PW2_NSLOT == 2) {
+            if (c == 0)
+                w2_sync<NST>(active);
+            else
+                w2_sync<0>(active);
+        } else {
+            w2_sync_n(w2_pieces(S, P.c + 2, wave) + (c == 0 ? NST : 0), active);
+        }
+        w2_stage(pk, S, P.c + PW2_NSLOT, P.slot(P.c), wave, lane);
         asm volatile("" ::: "memory");
         ++P.c;
     }
@@ -1099,9 +1125,8 @@ PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sche
     const bool active = blockIdx.x * PW2_PTS + wave * 32 < Npad; /* wave-uniform */               \
     const size_t boff = (size_t)b * Npad * CH;                                                    \
     W2Pipe P{w2smem, 0};                                                                          \
-    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);                                 \
-    w2_stage(pk, S, 0, P.slot(0), wave, lane);                                                    \
-    w2_stage(pk, S, 1, P.slot(1), wave, lane);
+    float *cf = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);                         \
+    for (int c_ = 0; c_ < PW2_NSLOT; ++c_) w2_stage(pk, S, c_, P.slot(c_), wave, lane);
 
 // layer0 (Conv1d in_dim -> 128 on exact fp32 MFMA 32x32x2, k-step j: inputs 2j + h)
 // + PointCN_0 + QKV_0.
@@ -1185,9 +1210,8 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
     // the K/V ring is free (the core ends on a barrier): weight chunks 0, 1 and the coefficients
     W2Pipe P{w2smem, 0};
-    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);
-    w2_stage(pk, S, 0, P.slot(0), wave, lane);
-    w2_stage(pk, S, 1, P.slot(1), wave, lane);
+    float *cf = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
+    for (int c = 0; c < PW2_NSLOT; ++c) w2_stage(pk, S, c, P.slot(c), wave, lane);
     w2_coef_mid(cf, pk, m, d, tid);
     f16x8 xh[8], xl[8];
     if (active) w2_msg_frags(O, l_run, xh, xl);  // msg = O / l
@@ -1324,9 +1348,8 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_last_kernel(
     float m_run, l_run;
     attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
     W2Pipe P{w2smem, 0};
-    float *cf = reinterpret_cast<float *>(w2smem + 2 * PW2_SLOT);
-    w2_stage(pk, S, 0, P.slot(0), wave, lane);
-    w2_stage(pk, S, 1, P.slot(1), wave, lane);
+    float *cf = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
+    for (int c = 0; c < PW2_NSLOT; ++c) w2_stage(pk, S, c, P.slot(c), wave, lane);
     w2_coef_last(cf, pk, m, c0, c2, c4w, tid);
     f16x8 xh[8], xl[8];
     if (active) w2_msg_frags(O, l_run, xh, xl);
