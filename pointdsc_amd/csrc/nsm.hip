@@ -242,13 +242,14 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
 #pragma unroll
         for (int i = 0; i < NI; ++i)
             if (J(i) < N) lmin = min(lmin, K(i));
-        uint32_t lrank = 0;
-        for (int t = 0; t < 64; ++t) {
-            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)lmin, t);
-            lrank += (o < lmin) || (o == lmin && t < lane);
+        // tau0 = the want-th smallest lane minimum: the smallest value v with
+        // #{lanes: lmin <= v} >= want, built bit by bit from the top (one
+        // compare + ballot + scalar popcount per bit instead of 64 readlanes)
+        uint32_t tau0 = 0;
+        for (int bit = 31; bit >= 0; --bit) {
+            const uint32_t probe = tau0 | ((1u << bit) - 1u);  // this bit 0, all lower bits 1
+            if ((uint32_t)__popcll(__ballot(lmin <= probe)) < want) tau0 |= 1u << bit;
         }
-        const unsigned long long hitm = __ballot(lrank == want - 1);
-        const uint32_t tau0 = (uint32_t)__shfl((int)lmin, __ffsll(hitm) - 1);
         const unsigned long long below = (1ull << lane) - 1ull;
         uint32_t c = 0;
 #pragma unroll
