@@ -187,8 +187,12 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
     return mfma_h(wh, xh, c);
 }
 
+// K/V ring slots: 2, or 3 for the staggered 8-wave schedule (V of the
+// previous tile is still being read by the late half)
 template <int NW>
-constexpr size_t attention_h3_lds_bytes() { return (size_t)2 * (H3_KTB + H3_VTB); }
+constexpr int h3_ring_slots() { return NW >= 8 ? 3 : 2; }
+template <int NW>
+constexpr size_t attention_h3_lds_bytes() { return (size_t)h3_ring_slots<NW>() * (H3_KTB + H3_VTB); }
 
 PDSC_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
@@ -336,7 +340,8 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // no faster: DESIGN.md §7.)
     // (the tile's V exponent is a vector load issued with the M loads: a scalar
     // load here is waited for with lgkmcnt(0) in the middle of the softmax)
-    auto tile = [&](const char *Kl, const char *Vl, int key0, float (&mv)[16], float ev) {
+    // QK^T + online softmax of one key tile -> this lane's P fragments (ph, pl)
+    auto qk_softmax = [&](const char *Kl, int key0, float (&mv)[16], float ev, f16x8(&ph)[2], f16x8(&pl)[2]) {
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
         f16x8 kf[3][2];
@@ -376,7 +381,6 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         }
         const float mb = m_run - (float)H3_PSHIFT + ev;
         float psum = 0.0f;
-        f16x8 ph[2], pl[2];
         float ex[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -391,7 +395,9 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             split8x(v, ph[s], pl[s]);
         }
         l_run += ldexpf(psum, (int)ev);
-        // O^T[32 t + m][query] += sum_key V[key][32 t + m] P[query][key]
+    };
+    // O^T[32 t + m][query] += sum_key V[key][32 t + m] P[query][key]
+    auto pv = [&](const char *Vl, const f16x8(&ph)[2], const f16x8(&pl)[2]) {
         f16x8 vf[3][2];
         auto vread = [&](int i, f16x8(&f)[2]) {  // fragment i = (t, s) = (i / 2, i % 2)
             f[0] = *reinterpret_cast<const f16x8 *>(Vl + 2 * h3_frag(i, 0, lane));
@@ -425,18 +431,53 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // included, because it does not count LDS-DMA -- issued at the tile start
     // or at the end of the previous tile: no faster, and the compiler copies
     // asm-loaded registers before the wait.  DESIGN.md section 7.)
+    constexpr int NSL = h3_ring_slots<NW>();
+    auto slot_base = [&](int st) { return h3smem + ((st - st0) % NSL) * (H3_KTB + H3_VTB); };
     if (st0 < st1) stage(st0, 0);
     sync();
-    for (int st = st0; st < st1; ++st) {
-        const int slot = (st - st0) & 1;
-        float mv[16], ev;
-        load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
-        if (st + 1 < st1) stage(st + 1, slot ^ 1);
-        {  // padding waves (q0 >= Npad) compute on clamped operands and store nothing
-            const char *base = h3smem + slot * (H3_KTB + H3_VTB);
-            tile(base, base + H3_KTB, st * H3_TILE, mv, ev);
+    if constexpr (NW < 8) {
+        for (int st = st0; st < st1; ++st) {
+            float mv[16], ev;
+            f16x8 ph[2], pl[2];
+            load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
+            if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
+            // padding waves (q0 >= Npad) compute on clamped operands and store nothing
+            qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
+            pv(slot_base(st) + H3_KTB, ph, pl);
+            sync();
         }
-        sync();
+    } else {
+        // 8 waves, two per SIMD (waves w and w + 4 share one): the second half
+        // runs each tile's PV one half-tile late, so on every SIMD one wave's
+        // QK^T + softmax (MFMA then VALU) sits beside its partner's PV (MFMA)
+        // between the two barriers of a tile, and the other way round after
+        // the middle one.  Each wave's own order of operations is unchanged
+        // (bit-identical results); V of tile t - 1 stays in its ring slot for
+        // the late PV (3 slots).
+        const bool late = wave >= NW / 2;  // wave-uniform (SGPR)
+        f16x8 ph[2], pl[2];
+        for (int st = st0; st < st1; ++st) {
+            if (!late) {
+                float mv[16], ev;
+                load_m(st * H3_TILE, mv, ev);
+                if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
+                qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
+            } else {
+                if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
+                if (st > st0) pv(slot_base(st - 1) + H3_KTB, ph, pl);
+            }
+            __builtin_amdgcn_s_barrier();
+            if (!late) {
+                pv(slot_base(st) + H3_KTB, ph, pl);
+            } else {  // (M loaded here: not live beside the pending P fragments)
+                float mv[16], ev;
+                load_m(st * H3_TILE, mv, ev);
+                qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
+            }
+            sync();
+        }
+        if (late && st0 < st1) pv(slot_base(st1 - 1) + H3_KTB, ph, pl);
+        sync();  // the late half's last V reads are done before the ring is reused
     }
     l_run = halves_sum(l_run);
 }

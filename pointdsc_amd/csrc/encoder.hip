@@ -1390,7 +1390,7 @@ static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 
 // attn_pw2 wherever pw2 runs and the attention has one key split (knob
 // PDSC_FUSE=0 keeps the two launches; measurement only).
-static AttnGridH3 fused_grid(int B, int N) { return attention_h3_grid<PW2_W>(B, N, att_target()); }
+static AttnGridH3 fused_grid(int B, int N) { return attention_h3_grid<PW2_W>(B, N, att_target() * 4 / PW2_W); }
 bool attention_fused(int B, int N, bool f32) {
     static const bool off = [] {
         const char *e = getenv("PDSC_FUSE");
