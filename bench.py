@@ -58,13 +58,16 @@ def parse():
     ap.add_argument("--preset", default="3dmatch", choices=["3dmatch", "kitti"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--kernel-iters", type=int, default=20, help="launches per standalone-kernel timing (>= 1)")
     ap.add_argument("--f32-steps", type=int, default=3, help="steps of the exact-fp32 leg (0 = skip)")
     ap.add_argument("--path-n", type=int, default=5000, help="N of the compat+NSM path roofline (0 = skip)")
     ap.add_argument("--path-pairs", type=int, default=8)
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="exercise the multi-rank launch/gather plumbing on CPU (gloo), no forward")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.kernel_iters < 1 or a.steps < 1:
+        ap.error("--kernel-iters and --steps must be >= 1")
+    return a
 
 
 STAGES = ["compat", "encoder", "seeds", "seed_knn", "nsm", "hypotheses", "post_refine"]
