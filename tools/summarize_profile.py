@@ -101,6 +101,32 @@ def main(tag, src=None):
             for c, v in zip(extra, vals):
                 if v == v:
                     traffic[k[0]][str(k[1])][c] = v
+    need = {"SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES",
+            "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"}
+    if need <= set(extra):
+        # Derived (MI355X_MICROARCH.md constants table): SQ_BUSY_CYCLES summed over the
+        # 32 shader engines gives the effective clock over the dispatch; MFMA-busy
+        # cycles over (1024 SIMDs x those cycles) = the matrix pipes' busy fraction;
+        # SQ_WAIT_* and SQ_WAVE_CYCLES are both quad-cycle counts (their ratio is exact).
+        lines += ["", "Derived per dispatch (kernels >= 20 us): effective clock = SQ_BUSY_CYCLES / 32 SEs / "
+                  "duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x clock x duration); "
+                  "waits as fractions of SQ_WAVE_CYCLES.", "",
+                  "| kernel | grid | avg us | clock GHz | MFMA busy | VALU/MFMA instr | WAIT_ANY | WAIT_INST_ANY |",
+                  "|---|---|---|---|---|---|---|---|"]
+        for k in keys:
+            d = mean(dur[k])
+            if not d >= 20.0:
+                continue
+            m = {c: mean(pmc[k][c]) for c in need}
+            if any(v != v for v in m.values()):
+                continue
+            cyc = m["SQ_BUSY_CYCLES"] / 32.0
+            clk = cyc / (d * 1e3)
+            busy = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc) if cyc > 0 else float("nan")
+            ratio = m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"] if m["SQ_INSTS_MFMA"] > 0 else float("nan")
+            wc = m["SQ_WAVE_CYCLES"]
+            lines.append(f"| {k[0]} | {k[1]} | {d:.1f} | {clk:.2f} | {busy:.3f} | {ratio:.2f} | "
+                         f"{m['SQ_WAIT_ANY'] / wc:.2f} | {m['SQ_WAIT_INST_ANY'] / wc:.2f} |")
     open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
     print("\n".join(lines))
