@@ -677,11 +677,7 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
             acc[3] = __builtin_fmaf(trow[c + 3], vv[3], acc[3]);
         }
         float nv = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // (T v)_a  (bmm, :352)
-#ifdef NSM_XOR_SUM  // A/B build knob
-        const float nrm = sqrtf(wave_sum(nv * nv));
-#else
         const float nrm = sqrtf(wave_sum_dpp(nv * nv));  // no LDS round trip per iterate
-#endif
         nv = nv / (nrm + 1e-6f);                              // :353
         const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
         if (__all(close)) flags |= 1u << t;
