@@ -65,6 +65,9 @@ constexpr int H3_KTB = H3_TILE * H3_ROWB;    // K tile bytes (16 KiB)
 constexpr int H3_VTB = 2 * CH * H3_TILE * 2; // V tile bytes (16 KiB)
 constexpr int H3_PSHIFT = 7;                 // p = 2^(x - m + PSHIFT)
 constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by > 2^8
+#ifndef ATT_SOFTMAX_PRIO
+#define ATT_SOFTMAX_PRIO 1  // s_setprio of the softmax section (build knob; 0 = off)
+#endif
 constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8 (p * 2^-e stays >= 2^-24 of the sum)
 
 // The V-tile exponent for a tile whose max |v| is vmax: the largest e <= 8 with
@@ -357,6 +360,9 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             S = mfma_h3(kf[j % 3][0], kf[j % 3][1], qh[j], ql[j], S);
             __builtin_amdgcn_sched_barrier(0);
         }
+        // the softmax's VALU at raised issue priority (the partner wave on this
+        // SIMD is then mostly in its MFMA phase): -1.8 % per fused launch, measured
+        if (ATT_SOFTMAX_PRIO > 0) __builtin_amdgcn_s_setprio(ATT_SOFTMAX_PRIO);
         float p[16];
         float mx = -INFINITY;
 #pragma unroll
@@ -395,6 +401,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             split8x(v, ph[s], pl[s]);
         }
         l_run += ldexpf(psum, (int)ev);
+        if (ATT_SOFTMAX_PRIO > 0) __builtin_amdgcn_s_setprio(0);
     };
     // O^T[32 t + m][query] += sum_key V[key][32 t + m] P[query][key]
     auto pv = [&](const char *Vl, const f16x8(&ph)[2], const f16x8(&pl)[2]) {
