@@ -124,25 +124,15 @@ PDSC_DEV void split_h(float x, _Float16 &hi, _Float16 &lo) {
 // per value.  Inline asm: the inputs are the rounded fp32 values by
 // construction, and every use sees the same hi register.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <bool NOP = true>
 PDSC_DEV void split2(float x0, float x1, uint32_t &hi, uint32_t &lo) {
     asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(x0), "v"(x1));
     asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(x0), "v"(hi));
     // s_nop 1: the 2 wait states a VALU write needs before an MFMA reads the
     // register as A/B (hipcc pads nothing inside asm; the fragments often feed
     // the very next MFMA).  hi is 2+ instructions older than any MFMA here.
-#ifndef SPLIT_ONE_NOP
     asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1"
         : "+v"(lo)
         : "v"(x1), "v"(hi));
-#else  // A/B variant: volatile (asm order kept) so the padded pair stays last
-    if constexpr (NOP)
-        asm volatile("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1"
-                     : "+v"(lo)
-                     : "v"(x1), "v"(hi));
-    else
-        asm volatile("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(x1), "v"(hi));
-#endif
 }
 // 8 values (v[e] -> element e of the fragments)
 PDSC_DEV void split8x(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
@@ -150,15 +140,7 @@ PDSC_DEV void split8x(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         uint32_t a, b;
-#ifdef SPLIT_ONE_NOP  // A/B build knob: only the last pair pads (an MFMA reads the whole f16x8, so the
-                      // earlier pairs' registers are >= 3 VALU instructions old by then)
-        if (e == 3)
-            split2<true>(v[2 * e], v[2 * e + 1], a, b);
-        else
-            split2<false>(v[2 * e], v[2 * e + 1], a, b);
-#else
         split2(v[2 * e], v[2 * e + 1], a, b);
-#endif
         h[e] = a;
         l[e] = b;
     }
@@ -390,19 +372,8 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             for (int r = 0; r < 16; ++r)
                 if (key0 + acc_row(r, h) >= N) p[r] = -INFINITY;
         }
-#ifdef ATT_TREE  // A/B build knob: the tile max and row sum as balanced trees (shorter dependency chains)
-        {
-            float t8[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t8[i] = fmaxf(p[2 * i], p[2 * i + 1]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) t8[i] = fmaxf(t8[2 * i], t8[2 * i + 1]);
-            mx = fmaxf(fmaxf(t8[0], t8[1]), fmaxf(t8[2], t8[3]));
-        }
-#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, p[r]);
-#endif
         mx = halves_max(mx);
         if (__any(mx > m_run + H3_DEFER)) {  // wave-uniform re-base of the running max
             const float m_new = fmaxf(m_run, mx);
@@ -417,24 +388,11 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         const float mb = m_run - (float)H3_PSHIFT + ev;
         float psum = 0.0f;
         float ex[16];
-#ifdef ATT_TREE
-#pragma unroll
-        for (int r = 0; r < 16; ++r) ex[r] = __builtin_amdgcn_exp2f(p[r] - mb);
-        {
-            float t8[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t8[i] = ex[2 * i] + ex[2 * i + 1];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) t8[i] = t8[2 * i] + t8[2 * i + 1];
-            psum = (t8[0] + t8[1]) + (t8[2] + t8[3]);
-        }
-#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             ex[r] = __builtin_amdgcn_exp2f(p[r] - mb);
             psum += ex[r];
         }
-#endif
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             float v[8];
