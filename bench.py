@@ -118,7 +118,13 @@ def profiled(kernel, grid_threads):
     try:
         with open(path) as f:
             prof = json.load(f)
-        ent = prof["kernels"][kernel][str(grid_threads)]
+        ks = prof["kernels"]
+        # a templated kernel's rows are named with their arguments (nsm_seed_kernel<false, 48>):
+        # a bare name matches the one instantiation launched at this grid
+        names = [kernel] if kernel in ks else [k for k in ks if k.split("<")[0] == kernel and str(grid_threads) in ks[k]]
+        if len(names) != 1:
+            return None
+        ent = ks[names[0]][str(grid_threads)]
     except (OSError, KeyError, ValueError):
         return None
     return {"tag": prof["tag"], "hbm_bytes": ent.get("hbm_bytes"), "avg_ms": ent["avg_us"] / 1e3}
@@ -269,14 +275,18 @@ def main():
     from pointdsc_amd import kernels
     from pointdsc_amd import _lib
     from pointdsc_amd.PointDSC import PointDSC
-    from pointdsc_amd.synthetic import PRESETS, synthetic_batch, trained_state_dict
+    from pointdsc_amd.synthetic import BENCH_CLS, PRESETS, synthetic_batch, trained_state_dict
 
     p = PRESETS[args.preset]
     P, N = args.pairs, args.num_corr
     model = PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
                      inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40,
                      nms_radius=p["nms_radius"])
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict(args.preset).items()})
+    # the trained stand-in weights with the classifier rescaled so that every bench
+    # pair's seed ranking is tie-free (synthetic.BENCH_CLS): the headline workload is
+    # then pinned to the reference itself (tests/golden/bench_3dmatch_1k_tf.npz)
+    sd_bench = trained_state_dict(args.preset, 12, *BENCH_CLS)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_bench.items()})
     model = model.to(dev).eval()
     cfg, packed = model.pdsc_config(), model.packed_weights()
 
@@ -412,11 +422,9 @@ def main():
             nt5 = (N5 + 63) // 64
             shapes = [("compat_packed_kernel", nt5 * (nt5 + 1) // 2 * P5 * 256),
                       ("knn_dist_kernel", ((N5 + 31) // 32 + 4) // 5 * ((S5 + 127) // 128) * P5 * 256),
-                      ("split_rows_kernel", None),
-                      (f"knn_select_kernel<{next(r for r in (16, 32, 48, 64, 80, 96, 128, 0) if r == 0 or r * 64 >= N5)}>",
-                       (S5 + 3) // 4 * P5 * 256),
+                      ("knn_select_kernel", (S5 + 3) // 4 * P5 * 256),
                       ("nsm_seed_kernel", (S5 + 3) // 4 * P5 * 256), ("nsm_finish_kernel", S5 * P5 * 64)]
-            profs = [profiled(kname, g) for kname, g in shapes if g is not None]
+            profs = [profiled(kname, g) for kname, g in shapes]
             path_traffic = (sum(pr["hbm_bytes"] for pr in profs)
                             if profs and all(pr and pr["hbm_bytes"] is not None for pr in profs) else None)
             t_path = st5["compat"] + st5["seed_knn"] + st5["nsm"]
@@ -425,6 +433,8 @@ def main():
                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                              "traffic": path_traffic, "traffic_note": "HBM bytes of the stages' kernels per forward "
                              "(rocprofv3 2*FETCH_SIZE+WRITE_SIZE, profiles/traffic_current.json)",
+                             "traffic_achieved": path_traffic and round(path_traffic / (t_path * 1e-3) / 1e9, 1),
+                             "traffic_frac": path_traffic and round(path_traffic / (t_path * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                              "num_corr": N5, "pairs": P5, "path_ms": round(t_path, 4),
                              "bytes_per_pair": path_bytes(N5, S5, k5),
                              "stage_ms": {k: round(v, 4) for k, v in st5.items()},
@@ -477,6 +487,7 @@ def main():
             plan.run(corr, src, tgt)
             torch.cuda.synchronize(dev)
             t_lab, t_tr = plan.labels.clone(), plan.trans.clone()
+            f32_out = (plan32.trans.cpu().numpy(), plan32.labels.cpu().numpy())
             t0 = time.perf_counter()
             for _ in range(args.f32_steps):
                 plan32.run(corr, src, tgt)
@@ -489,10 +500,14 @@ def main():
             model.precision = "h3"
             del plan32, packed32
 
-        cpu = None
+        cpu = parity = None
         if not args.no_cpu_baseline and world == 1:
             from oracle import pdsc_oracle as O
-            sd_np = trained_state_dict(args.preset)
+            sd_np = sd_bench
+            hip_out = {"h3": (plan.trans.cpu().numpy(), plan.labels.cpu().numpy())}
+            if exact is not None:
+                hip_out["f32"] = f32_out
+            ref_out = []
             try:
                 from threadpoolctl import threadpool_info
                 cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
@@ -500,11 +515,25 @@ def main():
                 cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
             n_done, t_c = 0, time.perf_counter()
             while n_done < P and (n_done < 2 or time.perf_counter() - t_c < args.cpu_seconds):
-                O.forward_testing(data["corr_pos"][n_done], data["src_keypts"][n_done],
-                                  data["tgt_keypts"][n_done], sd_np, num_layers=12,
-                                  inlier_threshold=p["inlier_threshold"], nms_radius=p["nms_radius"])
+                r = O.forward_testing(data["corr_pos"][n_done], data["src_keypts"][n_done],
+                                      data["tgt_keypts"][n_done], sd_np, num_layers=12,
+                                      inlier_threshold=p["inlier_threshold"], nms_radius=p["nms_radius"])
+                ref_out.append((r["final_trans"], r["final_labels"]))
                 n_done += 1
             t_c = time.perf_counter() - t_c
+            # the headline pairs' outputs against the oracle (the cpu leg's own results):
+            # labels bit-exact, poses within north_star's 1e-4
+            parity = {"vs": "oracle.pdsc_oracle.forward_testing on the same pairs and weights (the oracle is "
+                            "pinned to the reference's outputs on all 128 bench pairs: "
+                            "tests/golden/bench_3dmatch_1k_tf.npz)", "pairs": n_done,
+                      "note": "poses beyond 1e-4 come from seed / kNN near-ties decided by fp32 rounding; "
+                              "tests/test_gpu_bench_parity.py pins the stages after them on the HIP path's own "
+                              "seeds and kNN rows at 1e-4"}
+            for mode, (tr, lab) in hip_out.items():
+                dT = [float(np.abs(tr[i] - ref_out[i][0]).max()) for i in range(n_done)]
+                eq = [bool(np.array_equal(lab[i], ref_out[i][1])) for i in range(n_done)]
+                parity[mode] = {"labels_equal_frac": sum(eq) / n_done, "max_pose_diff": max(dT),
+                                "pairs_pose_gt_1e-4": [i for i in range(n_done) if dT[i] > 1e-4]}
             cpu = {"value": round(n_done * N / t_c, 1), "unit": "correspondences/s", "cores": cores,
                    "kind": "port",
                    "sample": f"{n_done} of the {P} bench pairs (N={N}) through oracle.pdsc_oracle."
@@ -520,14 +549,15 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"synthetic random correspondences N={N} ({args.preset}-like, 30% inliers), "
                                    f"{P} scan pairs per GPU per step, full PointDSC testing forward "
-                                   f"(12 layers x 128 ch, trained synthetic weights)",
+                                   f"(12 layers x 128 ch, trained synthetic weights, classifier rescaled "
+                                   f"by synthetic.BENCH_CLS for tie-free seed ranking)",
                        "num_corr": N, "pairs_per_gpu_per_step": P, "global_batch": P * world,
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
-            "stages_ms": stages, "single_pair": single, "exact_f32": exact, "cpu_baseline": cpu,
+            "stages_ms": stages, "single_pair": single, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(result), flush=True)
     if grp:

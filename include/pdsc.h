@@ -179,8 +179,11 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
 /* ------------------------------------------------ a7-a8 NSM weights --------
  * Local k x k feature x spatial consistency (diag 0), power iteration with
  * the batch-global allclose early exit (rtol 1e-5, atol 1e-8, evaluated over
- * all S seeds of a pair, as torch.allclose does over the bs*S batch), then
- * w = v / (sum v + 1e-6).  Replaces models/PointDSC.py:257-282, :338-358.
+ * all B*S seeds of the call, as torch.allclose does over the bs*S batch of one
+ * cal_leading_eigenvector call), then w = v / (sum v + 1e-6); iters_used[b] is
+ * the same for every b.  Replaces models/PointDSC.py:257-282, :338-358.
+ * (pdsc_forward_testing exits per pair -- each pair is its own bs = 1 forward;
+ * pdsc_forward_training over the whole batch -- one reference forward.)
  * sigma_dev / sigma_d_dev: device scalars (learned sigma, sigma_spat).
  * weights [B,S,k]; iters_used [B] int32 (may be NULL); 1 <= k <= min(63, N-1).
  * precision: enum pdsc_precision (the feature Gram).  The workspace holds the
@@ -335,6 +338,20 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
                              float *final_trans, float *final_labels, float *conf_out,
                              int32_t *seeds_out, void *workspace, size_t workspace_bytes,
                              pdsc_stream_t stream);
+/* The same forward with the intermediates of every stage (no reference
+ * counterpart: the parity tests pin each stage on the forward's own values).
+ * Any member may be NULL.  k = min(cfg->k, N - 1), S = int(N * ratio).       */
+typedef struct pdsc_forward_debug {
+    float *conf;             /* [B,N] classifier logits (:171) */
+    int32_t *seeds;          /* [B,S] (:174) */
+    int32_t *knn;            /* [B,S,k] seed neighbourhoods (:250-252) */
+    float *weights;          /* [B,S,k] NSM weights (:280-282) */
+    float *trans_pre_refine; /* [B,4,4] the best hypothesis (:182) */
+} pdsc_forward_debug;
+int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                   const float *src, const float *tgt, int32_t B, int32_t N,
+                                   float *final_trans, float *final_labels, const pdsc_forward_debug *debug,
+                                   void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
 
 #ifdef __cplusplus
 }

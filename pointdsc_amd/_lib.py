@@ -49,6 +49,12 @@ def precision_code(precision) -> int:
 
 CFG = ctypes.POINTER(PdscConfig)
 
+
+class PdscForwardDebug(ctypes.Structure):
+    """``struct pdsc_forward_debug`` (include/pdsc.h): optional stage outputs."""
+    _fields_ = [("conf", vp), ("seeds", vp), ("knn", vp), ("weights", vp), ("trans_pre_refine", vp)]
+
+
 # name -> (restype, argtypes)
 _PROTOS = {
     "pdsc_version": (ctypes.c_char_p, []),
@@ -92,6 +98,8 @@ _PROTOS = {
     "pdsc_forward_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_forward_testing": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp,
                                        c_size_t, vp]),
+    "pdsc_forward_testing_debug": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp,
+                                             ctypes.POINTER(PdscForwardDebug), vp, c_size_t, vp]),
     "pdsc_ply_read_xyz": (c_int32, [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "pdsc_radius_knn_workspace_bytes": (c_size_t, [c_int32]),
     "pdsc_radius_knn": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, vp, c_size_t, vp]),

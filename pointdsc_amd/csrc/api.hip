@@ -187,7 +187,7 @@ NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
 // f32: the Gram reads normed itself
 int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float *src, const float *tgt,
             const int *knn, int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d,
-            const NsmBufs &nb, float *weights, int *iters, hipStream_t s) {
+            const NsmBufs &nb, float *weights, int *iters, bool batch_global, hipStream_t s) {
     if (!f32 && !normed_s) {
         HIPCHK(launch_split_rows(normed, (size_t)B * N, nb.ns, s));
         normed_s = nb.ns;
@@ -195,7 +195,7 @@ int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float
     const void *feats = f32 ? static_cast<const void *>(normed) : static_cast<const void *>(normed_s);
     if (T > 0)
         HIPCHK(launch_nsm_seed(feats, f32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
-    HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, weights, iters, s));
+    HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, batch_global, weights, iters, s));
     return PDSC_OK;
 }
 
@@ -540,7 +540,7 @@ int32_t pdsc_nsm_weights(const float *normed, const float *src, const float *tgt
     Carve c(ws);
     NsmBufs nb = carve_nsm(c, B, N, S, k, T, true);
     return run_nsm(normed, nullptr, precision == PDSC_PRECISION_F32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d,
-                   nb, weights, iters, S_(stream));
+                   nb, weights, iters, true, S_(stream));
 }
 
 // -------------------------------------------------------------------- a9
@@ -600,6 +600,19 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
                              const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
                              float *final_labels, float *conf_out, int32_t *seeds_out, void *ws,
                              size_t ws_bytes, pdsc_stream_t stream) {
+    pdsc_forward_debug dbg{};
+    dbg.conf = conf_out;
+    dbg.seeds = seeds_out;
+    return pdsc_forward_testing_debug(cfg, packed, corr_pos, src, tgt, B, N, final_trans, final_labels, &dbg, ws,
+                                      ws_bytes, stream);
+}
+
+int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                   const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
+                                   float *final_labels, const pdsc_forward_debug *dbg, void *ws, size_t ws_bytes,
+                                   pdsc_stream_t stream) {
+    const pdsc_forward_debug no{};
+    if (!dbg) dbg = &no;
     RET_IF(check_cfg(cfg));
     Dims d;
     RET_IF(make_dims(cfg, B, N, d));
@@ -636,22 +649,27 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
     RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
     STAGE(4);
     // a7-a8 (:257-282)
+    // per pair: each pair is its own bs = 1 forward, whose allclose spans its S seeds
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
-                   nullptr, s));
+                   nullptr, false, s));
     STAGE(5);
     // a9-a10 (:287-335)
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
                              f.seed_trans, f.counts, f.hsums, s));
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
                               nullptr, nullptr, final_trans, final_labels, s));
+    if (dbg->trans_pre_refine)
+        HIPCHK(hipMemcpyAsync(dbg->trans_pre_refine, final_trans, sizeof(float) * 16 * d.B, hipMemcpyDeviceToDevice, s));
     STAGE(6);
     // a11 (:186, :403-438)
     HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s));
     STAGE(7);
 #undef STAGE
-    if (conf_out) HIPCHK(hipMemcpyAsync(conf_out, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
-    if (seeds_out)
-        HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    if (dbg->conf) HIPCHK(hipMemcpyAsync(dbg->conf, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
+    if (dbg->seeds) HIPCHK(hipMemcpyAsync(dbg->seeds, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    if (dbg->knn) HIPCHK(hipMemcpyAsync(dbg->knn, f.knn, sizeof(int) * d.B * d.S * d.k, hipMemcpyDeviceToDevice, s));
+    if (dbg->weights)
+        HIPCHK(hipMemcpyAsync(dbg->weights, f.weights, sizeof(float) * d.B * d.S * d.k, hipMemcpyDeviceToDevice, s));
     return PDSC_OK;
 }
 
@@ -692,8 +710,9 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     // a6-a10 as in testing (:182 -> cal_seed_trans), no post-refinement (:185-186)
     // (f.counts: the hypotheses' inlier counts later, the overflow flags here)
     RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
+    // the training batch is ONE reference forward: torch.allclose over all B * S seeds (:354)
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm,
-                   f.weights, nullptr, s));
+                   f.weights, nullptr, true, s));
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold, f.seed_trans,
                              f.counts, f.hsums, s));
     // the labels of the best hypothesis are not returned in training mode (:189-191): f.lm is scratch

@@ -8,7 +8,7 @@
 //   nsm_seed     a7-a8  one wave per seed: k x k feature Gram on the fp16
 //                    matrix cores (3-product split), T = F o S in LDS, then all
 //                    num_iterations power iterates + per-iterate allclose flags
-//   nsm_finish   a8  pair-global early exit t* = first iterate where every seed
+//   nsm_finish   a8  pair- or batch-global early exit t* = first iterate where every seed
 //                    is allclose (torch.allclose over the whole batch, :354)
 //   hypotheses   a9-a10  weighted Kabsch per seed (fp64 3x3 SVD on device) +
 //                    inlier count over all N correspondences
@@ -858,14 +858,16 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
 // w = v_{t*} / (sum v_{t*} + 1e-6)  (models/PointDSC.py:280-282)
 __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict__ hist,
                                                         const unsigned *__restrict__ seed_flags, int S,
-                                                        int k, int T, float *__restrict__ weights,
+                                                        int k, int T, int batch_global, float *__restrict__ weights,
                                                         int *__restrict__ iters_used) {
     const int b = blockIdx.y, s = blockIdx.x, a = threadIdx.x;
-    // the pair-global allclose bits: AND over the pair's S seeds (torch.allclose
-    // over the pair's [S, k] iterate, :354)
+    // the allclose bits ANDed over the seeds torch.allclose sees at once (:354):
+    // the pair's S seeds (a bs = 1 testing forward) or, batch_global, all
+    // gridDim.y * S seeds of the call (the training forward's [bs * S, k] iterate)
+    const size_t q0 = batch_global ? 0 : (size_t)b * S, nq = batch_global ? (size_t)gridDim.y * S : (size_t)S;
     unsigned all = 0xffffffffu;
     if (T > 0)
-        for (int q = a; q < S; q += 64) all &= seed_flags[(size_t)b * S + q];
+        for (size_t q = a; q < nq; q += 64) all &= seed_flags[q0 + q];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) all &= (unsigned)__shfl_xor((int)all, o);
     const unsigned m = all & ((T >= 32) ? 0xffffffffu : ((1u << T) - 1u));
@@ -879,8 +881,8 @@ __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict_
 }
 
 hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T,
-                             float *weights, int *iters_used, hipStream_t s) {
-    hipLaunchKernelGGL(nsm_finish_kernel, dim3(S, B), dim3(64), 0, s, hist, seed_flags, S, k, T,
+                             bool batch_global, float *weights, int *iters_used, hipStream_t s) {
+    hipLaunchKernelGGL(nsm_finish_kernel, dim3(S, B), dim3(64), 0, s, hist, seed_flags, S, k, T, (int)batch_global,
                        weights, iters_used);
     return hipGetLastError();
 }

@@ -199,7 +199,7 @@ hipError_t launch_seed_knn_fused(const _Float16 *ns, const int *seeds, int B, in
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
                            int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
                            unsigned *seed_flags, hipStream_t s);
-hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T,
+hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T, bool batch_global,
                              float *weights, int *iters_used, hipStream_t s);
 // sums: scratch [B][S][15]
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,

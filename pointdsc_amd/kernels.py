@@ -255,6 +255,33 @@ def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
     return trans, labels
 
 
+def forward_stages(cfg, packed, corr_pos, src, tgt):
+    """The full testing forward for B pairs with every stage's output
+    (pdsc_forward_testing_debug): dict of final_trans [B,4,4], final_labels
+    [B,N], conf [B,N], seeds [B,S], knn [B,S,k], weights [B,S,k],
+    trans_pre_refine [B,4,4] (int32 indices)."""
+    corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
+    B, N, _ = src.shape
+    _check_inputs(cfg, corr_pos, src, tgt)
+    dev = src.device
+    L = _lib.load()
+    nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
+    if nb == 0:
+        raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
+    ws = _workspace(nb, dev)
+    S, k = int(N * cfg.ratio), min(cfg.k, N - 1)
+    f32, i32 = dict(dtype=torch.float32, device=dev), dict(dtype=torch.int32, device=dev)
+    out = {"final_trans": torch.empty((B, 4, 4), **f32), "final_labels": torch.empty((B, N), **f32),
+           "conf": torch.empty((B, N), **f32), "seeds": torch.empty((B, S), **i32),
+           "knn": torch.empty((B, S, k), **i32), "weights": torch.empty((B, S, k), **f32),
+           "trans_pre_refine": torch.empty((B, 4, 4), **f32)}
+    dbg = _lib.PdscForwardDebug(*(out[n].data_ptr() for n in ("conf", "seeds", "knn", "weights", "trans_pre_refine")))
+    check(L.pdsc_forward_testing_debug(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
+                                       _p(out["final_trans"]), _p(out["final_labels"]), ctypes.byref(dbg), _p(ws), nb,
+                                       _stream(dev)), "pdsc_forward_testing_debug")
+    return out
+
+
 def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=False):
     """Training-mode forward (models/PointDSC.py:158-163, :176, :182, :189-191) for
     B pairs: (final_trans [B,4,4], confidence [B,N], M [B,N,N] | None,

@@ -149,6 +149,15 @@ def synthetic_state_dict(num_layers: int = 12, num_channels: int = 128, in_dim: 
     return sd
 
 
+# bench.py's classifier rescale (shift, scale) of the trained stand-in weights: the
+# unscaled logits of the bench pairs reach -460 and are all negative on some pairs,
+# where pick_seeds' ranking (models/PointDSC.py:216-217) is decided by the order of
+# tied zero scores -- arbitrary in torch's argsort.  logit / 32 + 15
+# lies in [0.6, 16] on all 128 bench pairs (tests/golden/bench_3dmatch_1k_tf.npz):
+# the same NMS and seed order wherever the unscaled ranking is tie-free.
+BENCH_CLS = (15.0, 2.0 ** -5)
+
+
 def trained_weights_path(preset: str = "3dmatch") -> str:
     """The synthetic stand-in checkpoint trained by tools/train_synthetic.py."""
     import os

@@ -18,7 +18,7 @@ def pytest_configure(config):
 
 def golden_names():
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and not f.startswith(("weights_", "kabsch_", "train_")))
+                  if f.endswith(".npz") and not f.startswith(("weights_", "kabsch_", "train_", "bench_")))
 
 
 def load_golden(name):

@@ -203,7 +203,8 @@ def run_training(name, L, N, B, preset, pseed, ratio):
     from libs.loss import SpectralMatchingLoss
     torch.set_num_threads(1)
     p = PRESETS[preset]
-    pairs = [synthetic_pair(N, pseed * 1000 + b, preset, ratio) for b in range(B)]
+    ratios = ratio if isinstance(ratio, tuple) else (ratio,) * B
+    pairs = [synthetic_pair(N, pseed * 1000 + b, preset, ratios[b]) for b in range(B)]
     sd_np = trained_state_dict(preset, L, 10.0, 1.0)  # classifier shift: distinct positive logits
     model = refmod.PointDSC(in_dim=6, num_layers=L, num_channels=128, num_iterations=10, ratio=0.1,
                             inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40,
@@ -227,7 +228,7 @@ def run_training(name, L, N, B, preset, pseed, ratio):
         loss_b = SpectralMatchingLoss(balanced=True)(res["M"], gt).item()
         loss_u = SpectralMatchingLoss(balanced=False)(res["M"], gt).item()
     M = res["M"].numpy()
-    out = dict(num_layers=L, preset=preset, pair_seed=pseed, inlier_ratio=ratio, weights_sha256=weights_digest(sd_np),
+    out = dict(num_layers=L, preset=preset, pair_seed=pseed, inlier_ratio=np.array(ratios), weights_sha256=weights_digest(sd_np),
                cls_bias_shift=10.0, cls_scale=1.0, sigma_d=p["sigma_d"], inlier_threshold=p["inlier_threshold"],
                nms_radius=p["nms_radius"],
                corr_pos=data["corr_pos"].numpy(), src_keypts=data["src_keypts"].numpy(),
@@ -244,8 +245,69 @@ def run_training(name, L, N, B, preset, pseed, ratio):
           f"{os.path.relpath(path, REPO)} ({os.path.getsize(path) / 1e3:.0f} kB)")
 
 
+def run_bench(preset="3dmatch", P=128, N=1000, shift=0.0, scale=1.0):
+    """The reference's testing forward on bench.py's own headline pairs: pair g
+    seeded 1000*100003+g (bench.py), N=1000, the UNSHIFTED trained synthetic
+    weights (classifier shift/scale as trained_state_dict; bench.py's tie-free
+    variant BENCH_CLS = (15, 2^-5) puts every logit of these pairs in [0.6, 16]).
+    Stores per pair: final_trans, final_labels, confidence, is_local_max, seeds
+    and the seed-ranking tie margins (seed scores are conf * is_local_max,
+    models/PointDSC.py:216-217: with negative logits the zero scores of
+    non-maxima tie), so the GPU tests can tell a genuine pose
+    error from a tie the reference breaks arbitrarily."""
+    import torch
+    sys.path.insert(0, REF)
+    import models.PointDSC as refmod
+    torch.set_num_threads(os.cpu_count())
+    p = PRESETS[preset]
+    sd_np = trained_state_dict(preset, 12, shift, scale)
+    model = refmod.PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
+                            inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40,
+                            nms_radius=p["nms_radius"])
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
+    model.eval()
+    rec = {}
+    o_pick = model.pick_seeds
+
+    def pick_wrap(dists, scores, R, max_num):
+        s = o_pick(dists, scores, R, max_num)
+        rec["seeds"] = s.clone()
+        rec["is_local_max"] = ((scores.T >= scores) | (dists[0] >= R)).min(-1)[0].float().clone()
+        return s
+
+    model.pick_seeds = pick_wrap
+    hook = model.classification.register_forward_hook(lambda m, i, o: rec.__setitem__("conf", o.clone()))
+    keys = ("final_trans", "final_labels", "confidence", "is_local_max", "seeds")
+    out = {k: [] for k in keys}
+    for g in range(P):
+        pair = synthetic_pair(N, 1000 * 100003 + g, preset)
+        data = {k: torch.from_numpy(pair[k])[None] for k in ("corr_pos", "src_keypts", "tgt_keypts")}
+        data["testing"] = True
+        with torch.no_grad():
+            res = model(data)
+        out["final_trans"].append(res["final_trans"][0].numpy())
+        out["final_labels"].append(res["final_labels"][0].numpy().astype(np.uint8))
+        out["confidence"].append(rec["conf"][0, 0].numpy())
+        out["is_local_max"].append(rec["is_local_max"].numpy().astype(np.uint8))
+        out["seeds"].append(rec["seeds"][0].numpy().astype(np.int32))
+    hook.remove()
+    out = {k: np.stack(v) for k, v in out.items()}
+    sc = out["confidence"] * out["is_local_max"]
+    out["n_nonpositive_seed_scores"] = np.array([(sc[g][out["seeds"][g]] <= 0).sum() for g in range(P)])
+    tag = f"bench_{preset}_{N // 1000}k" + ("_tf" if shift else "")
+    path = os.path.join(REPO, "tests", "golden", f"{tag}.npz")
+    np.savez_compressed(path, preset=preset, num_corr=N, pairs=P, cls_bias_shift=shift, cls_scale=scale,
+                        pair_seed_base=1000 * 100003, weights_sha256=weights_digest(sd_np), **out)
+    print(f"{tag}: {P} pairs, pairs with non-positive seed scores: "
+          f"{int((out['n_nonpositive_seed_scores'] > 0).sum())} -> {os.path.relpath(path, REPO)} "
+          f"({os.path.getsize(path) / 1e3:.0f} kB)")
+
+
 TRAIN_CASES = {"small": (2, 256, 2, "3dmatch", 41, 0.3), "rel_1k": (12, 1000, 2, "3dmatch", 42, 0.3),
-               "kitti_1k": (12, 1000, 1, "kitti", 43, 0.2)}
+               "kitti_1k": (12, 1000, 1, "kitti", 43, 0.2),
+               # pairs that converge after different numbers of power iterations: the
+               # batch-global allclose exit (models/PointDSC.py:354) differs from a per-pair one
+               "mix": (12, 400, 6, "3dmatch", 44, (0.0, 0.05, 0.3, 0.6, 0.9, 0.15))}
 
 
 def run_kabsch():
@@ -295,6 +357,10 @@ if __name__ == "__main__":
     for n in names:
         if n == "kabsch":
             run_kabsch()
+        elif n.startswith("bench_"):  # bench_<preset>[_tf]: the bench's weights [tie-free variant]
+            from pointdsc_amd.synthetic import BENCH_CLS
+            parts = n.split("_")
+            run_bench(parts[1], **(dict(shift=BENCH_CLS[0], scale=BENCH_CLS[1]) if parts[-1] == "tf" else {}))
         elif n.startswith("train_"):
             run_training(n[6:], *TRAIN_CASES[n[6:]])
         else:
