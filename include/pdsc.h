@@ -157,7 +157,8 @@ int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *coun
  * pick_seeds: radius NMS on the confidences then the top-S of
  * conf * is_local_max in descending order (ties: ascending index).
  * Replaces models/PointDSC.py:199-217.  src [B,N,3]; conf [B,N];
- * seeds [B,S] int32; is_local_max [B,N] (0/1 fp32, may be NULL).           */
+ * seeds [B,S] int32; is_local_max [B,N] (0/1 fp32; required, it hosts the
+ * flags between the two launches).                                          */
 int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t N, float radius,
                         int32_t S, int32_t *seeds, float *is_local_max, pdsc_stream_t stream);
 
@@ -168,9 +169,7 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
  * Replaces models/common.py:48-69 + models/PointDSC.py:250-252 (only the
  * S seed rows are computed).  normed [B,N,C]; seeds [B,S]; knn [B,S,k];
  * 1 <= k <= 63, k + 1 <= N.  precision: enum pdsc_precision (distances).
- * The workspace holds the [B,S,N] distance rows (H3 opt-in PDSC_KNN_FUSED=1:
- * one fused launch that writes them only for seeds whose tie group overflows
- * its candidate lists).                                                      */
+ * The workspace holds the [B,S,N] distance rows.                            */
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S);
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
                       int32_t S, int32_t k, int32_t precision, int32_t *knn, void *workspace,

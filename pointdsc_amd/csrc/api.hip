@@ -442,6 +442,8 @@ int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *coun
 }
 
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *Npad, int32_t *nsplit) {
+    if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision %d (enum pdsc_precision)", precision);
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
     *nsplit = attention_nsplit(B, N, precision == PDSC_PRECISION_F32);
@@ -449,6 +451,8 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *
 }
 
 int32_t pdsc_encoder_plan(int32_t B, int32_t N, int32_t precision, int32_t *fused) {
+    if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
+        return fail(PDSC_ERR_ARG, "precision %d (enum pdsc_precision)", precision);
     if (B < 1 || N < 1 || !fused) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *fused = attention_fused(B, N, precision == PDSC_PRECISION_F32) ? 1 : 0;
     return PDSC_OK;
@@ -466,27 +470,12 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
 }
 
 // -------------------------------------------------------------------- a6
-// H3 seed kNN: knn_dist + knn_select (default), or knn_fused_kernel with the knob
-// PDSC_KNN_FUSED=1 (bit-identical; measured 1.9x / 2.2x SLOWER at N = 1000 / 5000:
-// each wave ranks 8 seeds' candidates serially and sweeps its key tiles with a
-// one-tile register prefetch, both latency-bound -- DESIGN.md section 7)
-static bool knn_fused_on() {
-    static const bool on = [] {
-        const char *e = getenv("PDSC_KNN_FUSED");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 // a6 (:250-252) for the forwards: knn [B][S][k]; dist [B][S][N] and redo [B][S] scratch
 int run_seed_knn(const float *normed, const _Float16 *normed_s, bool f32, const int *seeds, int B, int N, int S,
                  int k, float *dist, int *redo, int *knn, hipStream_t s) {
     HIPCHK(hipMemsetAsync(knn, 0, sizeof(int) * B * S * k, s));
     if (f32) {
         HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s));
-    } else if (knn_fused_on()) {
-        HIPCHK(launch_seed_knn_fused(normed_s, seeds, B, N, S, k, dist, knn, redo, s));
-        return PDSC_OK;
     } else {
         HIPCHK(launch_knn_dist(normed_s, seeds, B, N, S, dist, s));
     }

@@ -122,17 +122,19 @@ PDSC_DEV void split_h(float x, _Float16 &hi, _Float16 &lo) {
 // exact difference of the fp32 value and the fp16 hi operand and round once --
 // bit-identical to split_h (x - hi is exact in fp32), 1.5 instead of ~2.5 VALU
 // per value.  Inline asm: the inputs are the rounded fp32 values by
-// construction, and every use sees the same hi register.
+// construction, and every use sees the same hi register.  ONE asm statement:
+// the closing s_nop 1 gives both hi and lo the 2 wait states a VALU write needs
+// before an MFMA reads the register as A/B (hipcc pads nothing inside asm, and
+// its hazard recognizer does not see asm-written VGPRs); as separate statements
+// the scheduler could move the hi.hi MFMA right after the cvt.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 PDSC_DEV void split2(float x0, float x1, uint32_t &hi, uint32_t &lo) {
-    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hi) : "v"(x0), "v"(x1));
-    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(x0), "v"(hi));
-    // s_nop 1: the 2 wait states a VALU write needs before an MFMA reads the
-    // register as A/B (hipcc pads nothing inside asm; the fragments often feed
-    // the very next MFMA).  hi is 2+ instructions older than any MFMA here.
-    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\ts_nop 1"
-        : "+v"(lo)
-        : "v"(x1), "v"(hi));
+    asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+        "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %3, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+        "s_nop 1"
+        : "=&v"(hi), "=&v"(lo)
+        : "v"(x0), "v"(x1));
 }
 // 8 values (v[e] -> element e of the fragments)
 PDSC_DEV void split8x(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
@@ -190,12 +192,10 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
     return mfma_h(wh, xh, c);
 }
 
-// K/V ring slots: 2, or 3 for the staggered 8-wave schedule (V of the
-// previous tile is still being read by the late half)
+// K/V ring: 2 slots (tile t + 1 lands while tile t is consumed)
+constexpr int H3_NSLOT = 2;
 template <int NW>
-constexpr int h3_ring_slots() { return NW >= 8 ? 3 : 2; }
-template <int NW>
-constexpr size_t attention_h3_lds_bytes() { return (size_t)h3_ring_slots<NW>() * (H3_KTB + H3_VTB); }
+constexpr size_t attention_h3_lds_bytes() { return (size_t)H3_NSLOT * (H3_KTB + H3_VTB); }
 
 PDSC_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void *base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
@@ -438,59 +438,24 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // included, because it does not count LDS-DMA -- issued at the tile start
     // or at the end of the previous tile: no faster, and the compiler copies
     // asm-loaded registers before the wait.  DESIGN.md section 7.)
-    constexpr int NSL = h3_ring_slots<NW>();
-    auto slot_base = [&](int st) { return h3smem + ((st - st0) % NSL) * (H3_KTB + H3_VTB); };
+    auto slot_base = [&](int st) { return h3smem + ((st - st0) % H3_NSLOT) * (H3_KTB + H3_VTB); };
     if (st0 < st1) stage(st0, 0);
     sync();
-    if constexpr (NW < 8) {
-        for (int st = st0; st < st1; ++st) {
-            float mv[16], ev;
-            f16x8 ph[2], pl[2];
-            load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
-            if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
-            // padding waves (q0 >= Npad) compute on clamped operands and store nothing
-            qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
-            pv(slot_base(st) + H3_KTB, ph, pl);
-            sync();
-        }
-    } else {
-        // 8 waves, two per SIMD (waves w and w + 4 share one): the second half
-        // runs each tile's PV one half-tile late, so on every SIMD one wave's
-        // QK^T + softmax (MFMA then VALU) sits beside its partner's PV (MFMA)
-        // between the two barriers of a tile, and the other way round after
-        // the middle one.  Each wave's own order of operations is unchanged
-        // (bit-identical results); V of tile t - 1 stays in its ring slot for
-        // the late PV (3 slots).
-        const bool late = wave >= NW / 2;  // wave-uniform (SGPR)
+    for (int st = st0; st < st1; ++st) {
+        float mv[16], ev;
         f16x8 ph[2], pl[2];
-        for (int st = st0; st < st1; ++st) {
-            if (!late) {
-                float mv[16], ev;
-                load_m(st * H3_TILE, mv, ev);
-                if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
-                qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
-            } else {
-                if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % NSL));
-                if (st > st0) pv(slot_base(st - 1) + H3_KTB, ph, pl);
-            }
-            __builtin_amdgcn_s_barrier();
-            if (!late) {
-                pv(slot_base(st) + H3_KTB, ph, pl);
-            } else {  // (M loaded here: not live beside the pending P fragments)
-                float mv[16], ev;
-                load_m(st * H3_TILE, mv, ev);
-                qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
-            }
-            sync();
-        }
-        if (late && st0 < st1) pv(slot_base(st1 - 1) + H3_KTB, ph, pl);
-        sync();  // the late half's last V reads are done before the ring is reused
+        load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
+        if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
+        // padding waves (q0 >= Npad) compute on clamped operands and store nothing
+        qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
+        pv(slot_base(st) + H3_KTB, ph, pl);
+        sync();
     }
     l_run = halves_sum(l_run);
 }
 
 template <int NW, bool XCD, bool PACKED>
-__global__ __launch_bounds__(NW * 64, NW >= 8 ? 1 : 2) void attention_h3_kernel(
+__global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
     float *__restrict__ ml) {

@@ -748,9 +748,7 @@ constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 plan
 constexpr int PW2_SLOT = PW2_CB * PW2_BLKB;
 constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
-#ifndef PW2_NSLOT
-#define PW2_NSLOT 2  // weight-ring slots (A/B build knob: 3 = two chunks in flight)
-#endif
+constexpr int PW2_NSLOT = 2;                          // weight-ring slots
 constexpr size_t PW2_LDS = PW2_NSLOT * PW2_SLOT + PW2_COEF * sizeof(float);
 constexpr int W2_MAXCH = 24;
 
@@ -801,25 +799,6 @@ PDSC_DEV void w2_sync(bool active) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// w2_sync with a run-time count (wave-uniform): the 3-slot ring waits for chunk
-// c + 1 while chunk c + 2's pieces (and the caller's younger stores) stay in flight.
-#define W2_SYNC_CASE(n) \
-    case n: asm volatile("s_waitcnt vmcnt(" #n ") lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-PDSC_DEV void w2_sync_n(int n, bool active) {
-    n = __builtin_amdgcn_readfirstlane(active ? n : 0);
-    switch (n) {
-        W2_SYNC_CASE(1) W2_SYNC_CASE(2) W2_SYNC_CASE(3) W2_SYNC_CASE(4) W2_SYNC_CASE(5) W2_SYNC_CASE(6)
-        W2_SYNC_CASE(7) W2_SYNC_CASE(16) W2_SYNC_CASE(17) W2_SYNC_CASE(18) W2_SYNC_CASE(19) W2_SYNC_CASE(20)
-        W2_SYNC_CASE(21) W2_SYNC_CASE(22) W2_SYNC_CASE(23)
-        default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-}
-#undef W2_SYNC_CASE
-// this wave's LDS-DMA pieces of chunk c (w2_stage's loop count)
-PDSC_DEV int w2_pieces(const W2Sched &S, int c, int wave) {
-    return (c < S.n && S.np[c] > wave) ? (S.np[c] - wave + PW2_W - 1) / PW2_W : 0;
-}
-
 PDSC_DEV void w2_frag(const char *bp, f16x8 (&w)[3]) {
     w[0] = *reinterpret_cast<const f16x8 *>(bp);
     w[1] = *reinterpret_cast<const f16x8 *>(bp + 1024);
@@ -860,14 +839,10 @@ PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const W2Sched &S, const f16x8
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         if (active) w2_mma<NKS, NT, TRANS>(P.slot(P.c), xh, xl, acc, c * NT, lane);
-        if constexpr (PW2_NSLOT == 2) {
-            if (c == 0)
-                w2_sync<NST>(active);
-            else
-                w2_sync<0>(active);
-        } else {
-            w2_sync_n(w2_pieces(S, P.c + 2, wave) + (c == 0 ? NST : 0), active);
-        }
+        if (c == 0)
+            w2_sync<NST>(active);
+        else
+            w2_sync<0>(active);
         w2_stage(pk, S, P.c + PW2_NSLOT, P.slot(P.c), wave, lane);
         asm volatile("" ::: "memory");
         ++P.c;

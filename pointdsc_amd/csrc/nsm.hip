@@ -460,195 +460,6 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------ a6 fused
-// knn_fused_kernel<NW>: knn_dist + knn_select in one launch, the S x N
-// distance rows never stored.  A workgroup = 32 seeds of one pair (the seed
-// fragments of knn_dist_kernel, held for the launch) and NW waves; wave w sweeps
-// key tiles w, w + NW, ... with the next tile's key fragments loaded while the
-// current one's 24 MFMAs run.  The distances are the same MFMA chain as
-// knn_dist_kernel's (bit-identical).  Three phases:
-//  1. sweep: per (wave, lane, seed) the minimum key -> 32 NW group minima per
-//     seed; tau = the (k+1)-th smallest of the 64 per-lane minima of those
-//     (each of the k+1 smallest is a distinct correspondence, so at least k+1
-//     keys are <= tau: an upper bound on the (k+1)-th smallest distance)
-//  2. sweep again (MFMAs are cheap; the rows would be 4 S N bytes of HBM):
-//     every key <= tau is appended (LDS atomics) to its seed's candidate list
-//  3. rank the candidates by (key, index) -- the order knn_select_kernel
-//     ranks by -- and keep positions 1..k (:68 drops position 0)
-// A seed with more than KF_CAP candidates (heavy ties) is flagged in `redo`;
-// its distance row is then written by a third sweep and knn_select_kernel
-// re-runs on the flagged seeds alone.
-constexpr int KF_CAP = 128;
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 2) void knn_fused_kernel(const _Float16 *__restrict__ ns,
-                                                               const int *__restrict__ seeds, int N, int S, int k,
-                                                               float *__restrict__ dist, int *__restrict__ knn,
-                                                               int *__restrict__ redo) {
-    __shared__ uint32_t mins[32][NW * 32 + 1];
-    __shared__ uint32_t tau_s[32];
-    __shared__ int cnt[32];
-    __shared__ uint32_t ckey[32][KF_CAP];
-    __shared__ int cidx[32][KF_CAP];
-    __shared__ int over_s[32];
-    __shared__ f16x8 As[16][64];  // the seed fragments (k-step i: hi = 2 i, lo = 2 i + 1), lane-linear
-    const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int s0 = blockIdx.x * 32;
-    const _Float16 *F = ns + (size_t)b * N * 2 * CH;
-    if (wave == 0) {
-        const int sidx = s0 + l32;
-        const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
-        const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            As[2 * j][lane] = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * j + h));
-            As[2 * j + 1][lane] = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * j + h));
-        }
-    }
-    if (tid < 32) {
-        cnt[tid] = 0;
-        over_s[tid] = 0;
-    }
-    __syncthreads();
-    const int nkt = (N + 31) / 32;
-    auto kload = [&](int t, f16x8(&f)[16]) {  // key tile t's B fragments (row = key, chunk 2i + h)
-        const char *row = reinterpret_cast<const char *>(F + (size_t)min(t * 32 + l32, N - 1) * 2 * CH);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            f[2 * i] = *reinterpret_cast<const f16x8 *>(row + 16 * (2 * i + h));
-            f[2 * i + 1] = *reinterpret_cast<const f16x8 *>(row + 2 * CH + 16 * (2 * i + h));
-        }
-    };
-    // one sweep over this wave's key tiles, body(u = keys of the 16 seed rows, key index j)
-    auto sweep = [&](auto &&body) {
-        f16x8 k0[16], k1[16];
-        auto tile = [&](int t, const f16x8(&f)[16]) {
-            // the seed fragments re-read from LDS every tile: an opaque offset keeps
-            // the compiler from hoisting them into 64 loop-invariant VGPRs
-            int off = 16 * lane;
-            asm volatile("" : "+v"(off));
-            const char *ab = reinterpret_cast<const char *>(&As[0][0]) + off;
-            f32x16 acc = zero16();
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                acc = mfma_h3(*reinterpret_cast<const f16x8 *>(ab + 2048 * i),
-                              *reinterpret_cast<const f16x8 *>(ab + 2048 * i + 1024), f[2 * i], f[2 * i + 1], acc);
-            body(acc, t * 32 + l32);  // distance = 2 - 2 acc (as knn_dist_kernel)
-        };
-        if (wave < nkt) kload(wave, k0);
-        for (int t = wave; t < nkt; t += 2 * NW) {
-            if (t + NW < nkt) kload(t + NW, k1);
-            tile(t, k0);
-            if (t + 2 * NW < nkt) kload(t + 2 * NW, k0);
-            if (t + NW < nkt) tile(t + NW, k1);
-        }
-    };
-    // phase 1: group minima
-    uint32_t m[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) m[r] = 0xffffffffu;
-    sweep([&](const f32x16 &acc, int j) {
-        if (j < N) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) m[r] = min(m[r], fkey(2.0f - 2.0f * acc[r]));
-        }
-    });
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mins[acc_row(r, h)][wave * 32 + l32] = m[r];
-    __syncthreads();
-    const uint32_t want = k + 1;
-    for (int R = wave; R < 32; R += NW) {
-        if (s0 + R >= S) continue;  // wave-uniform
-        uint32_t lmin = 0xffffffffu;
-#pragma unroll
-        for (int q = 0; q < NW / 2; ++q) lmin = min(lmin, mins[R][lane + 64 * q]);
-        uint32_t lrank = 0;
-        for (int t = 0; t < 64; ++t) {
-            const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)lmin, t);
-            lrank += (o < lmin) || (o == lmin && t < lane);
-        }
-        const unsigned long long hitm = __ballot(lrank == want - 1);
-        if (lane == 0) tau_s[R] = (uint32_t)__builtin_amdgcn_readlane((int)lmin, __ffsll(hitm) - 1);
-    }
-    __syncthreads();
-    // phase 2: candidates
-    uint32_t tr[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tr[r] = tau_s[acc_row(r, h)];
-    sweep([&](const f32x16 &acc, int j) {
-        if (j < N) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const uint32_t u = fkey(2.0f - 2.0f * acc[r]);
-                if (u <= tr[r]) {
-                    const int R = acc_row(r, h);
-                    const int pos = atomicAdd(&cnt[R], 1);
-                    if (pos < KF_CAP) {
-                        ckey[R][pos] = u;
-                        cidx[R][pos] = j;
-                    }
-                }
-            }
-        }
-    });
-    __syncthreads();
-    // phase 3: rank by (key, index); positions 1..k
-    bool any_over = false;
-    for (int R = wave; R < 32; R += NW) {
-        const int s = s0 + R;
-        if (s >= S) continue;
-        const int c = cnt[R];
-        if (lane == 0) redo[(size_t)b * S + s] = c > KF_CAP;
-        if (c > KF_CAP) {
-            any_over = true;
-            if (lane == 0) over_s[R] = 1;
-            continue;
-        }
-        const int e0 = lane, e1 = lane + 64;
-        const uint32_t k0 = e0 < c ? ckey[R][e0] : 0xffffffffu;
-        const int i0 = e0 < c ? cidx[R][e0] : 0x7fffffff;
-        const uint32_t k1 = e1 < c ? ckey[R][e1] : 0xffffffffu;
-        const int i1 = e1 < c ? cidx[R][e1] : 0x7fffffff;
-        uint32_t r0 = 0, r1 = 0;
-        for (int q = 0; q < c; ++q) {
-            const uint32_t mu = ckey[R][q];
-            const int mi = cidx[R][q];
-            r0 += (mu < k0) || (mu == k0 && mi < i0);
-            r1 += (mu < k1) || (mu == k1 && mi < i1);
-        }
-        int *out = knn + ((size_t)b * S + s) * k;
-        if (e0 < c && r0 > 0 && r0 < want) out[r0 - 1] = i0;
-        if (e1 < c && r1 > 0 && r1 < want) out[r1 - 1] = i1;
-    }
-    // overflow (heavy ties): the flagged seeds' rows for knn_select_kernel
-    if (!__syncthreads_or(any_over)) return;
-    sweep([&](const f32x16 &acc, int j) {
-        if (j < N) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int R = acc_row(r, h);
-                if (s0 + R < S && over_s[R]) dist[((size_t)b * S + s0 + R) * N + j] = 2.0f - 2.0f * acc[r];
-            }
-        }
-    });
-}
-
-// H3 seed kNN (knn_fused_kernel, then knn_select_kernel on any overflow seeds);
-// dist: [B][S][N] scratch for those rows, redo: [B][S] flags.
-hipError_t launch_seed_knn_fused(const _Float16 *ns, const int *seeds, int B, int N, int S, int k, float *dist,
-                                 int *knn, int *redo, hipStream_t s) {
-    if (k < 1 || k > 63 || N < k + 1) return hipErrorInvalidValue;
-    const int nkt = (N + 31) / 32;
-    const dim3 grid((S + 31) / 32, B);
-    if (nkt <= 64)
-        hipLaunchKernelGGL(knn_fused_kernel<4>, grid, dim3(256), 0, s, ns, seeds, N, S, k, dist, knn, redo);
-    else
-        hipLaunchKernelGGL(knn_fused_kernel<8>, grid, dim3(512), 0, s, ns, seeds, N, S, k, dist, knn, redo);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_knn_select(dist, B, N, S, k, knn, s, redo);
-}
-
 // -------------------------------------------------------------- a7-a8 NSM
 constexpr int KMAX = 64;
 

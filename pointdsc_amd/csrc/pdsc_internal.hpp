@@ -190,10 +190,6 @@ hipError_t launch_knn_dist_f32(const float *normed, const int *seeds, int B, int
 // only: [B][S] flags, or null for every seed
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s,
                              const int *only = nullptr);
-// H3 seed kNN with the distance rows never stored (nsm.hip: knn_fused_kernel);
-// dist [B][S][N] is scratch for heavy-tie overflow rows, redo [B][S] ints.
-hipError_t launch_seed_knn_fused(const _Float16 *ns, const int *seeds, int B, int N, int S, int k, float *dist,
-                                 int *knn, int *redo, hipStream_t s);
 // feats: the split normed copy [B][N][2][128] fp16 (as launch_knn_dist reads it),
 // or the fp32 normed rows [B][N][128] when f32
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,

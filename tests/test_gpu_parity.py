@@ -542,51 +542,25 @@ def test_seed_knn_select_paths(k, dups, gpu_device):
         assert list(knn[0]) == list(ref[0])  # the tie group resolves by ascending index
 
 
-def _knn_cases():
-    """(name, f [B,N,128], seeds [B,S], k): both fused-kernel widths (N <= 2048:
-    4 waves, else 8), a batch, N % 32 != 0, k = 63, and a heavy tie group that
-    overflows the candidate lists (the knn_select re-run on flagged seeds)."""
-    out = []
-    for name, B, N, S, k, dups in [("b16_1k", 16, 1000, 100, 40, 0), ("b2_5k", 2, 5000, 500, 40, 0),
-                                   ("odd_777", 3, 777, 77, 63, 0), ("ties_3k", 1, 3000, 200, 40, 300)]:
-        rng = np.random.RandomState(N + B)
-        f = rng.randn(B, N, 128).astype(np.float32)
-        if dups:
-            f[:, 1000:1000 + dups] = f[:, 5:6]
-        f /= np.linalg.norm(f, axis=-1, keepdims=True)
-        seeds = np.stack([rng.choice(N, S, replace=False) for _ in range(B)]).astype(np.int32)
-        if dups:
-            seeds[:, 0], seeds[:, 1] = 5, 1000
-        out.append((name, f, seeds, k))
-    return out
-
-
-def _knn_outputs(device):
+@pytest.mark.parametrize("name,B,N,S,k,dups", [("b16_1k", 16, 1000, 100, 40, 0), ("b2_5k", 2, 5000, 500, 40, 0),
+                                                ("odd_777", 3, 777, 77, 63, 0), ("ties_3k", 1, 3000, 200, 40, 300)])
+def test_seed_knn_batched_cases(name, B, N, S, k, dups, gpu_device):
+    """The seed kNN (knn_dist + knn_select) on batches vs the oracle row by row: a
+    batch, N % 32 != 0 with k = 63, and a 300-point tie group (exact duplicate
+    features) that resolves by ascending index."""
+    from oracle import pdsc_oracle as O
     from pointdsc_amd import kernels
-    return {name: kernels.seed_knn(_t(f, device), _t(seeds, device, torch.int32), k).cpu().numpy()
-            for name, f, seeds, k in _knn_cases()}
-
-
-def _dump_knn_outputs(path):  # child process entry (PDSC_KNN_FUSED=1)
-    np.savez(path, **_knn_outputs(torch.device("cuda:0")))
-
-
-def test_fused_seed_knn_bit_identical(gpu_device, tmp_path):
-    """knn_fused_kernel (distances never stored; threshold, candidate lists,
-    (key, index) ranking; selected by the PDSC_KNN_FUSED=1 knob in the child
-    process) returns exactly the neighbours of the production knn_dist_kernel +
-    knn_select_kernel, including a tie group that overflows the candidate
-    lists and goes through the knn_select re-run."""
-    import os
-    import subprocess
-    import sys
-    ours = _knn_outputs(gpu_device)
-    out = tmp_path / "fused_knn.npz"
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, PDSC_KNN_FUSED="1")
-    code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
-           f"import test_gpu_parity as t; t._dump_knn_outputs({str(out)!r})"
-    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
-    ref = np.load(out)
-    for k, v in ours.items():
-        assert np.array_equal(v, ref[k]), k
+    rng = np.random.RandomState(N + B)
+    f = rng.randn(B, N, 128).astype(np.float32)
+    if dups:
+        f[:, 1000:1000 + dups] = f[:, 5:6]
+    f /= np.linalg.norm(f, axis=-1, keepdims=True)
+    seeds = np.stack([rng.choice(N, S, replace=False) for _ in range(B)]).astype(np.int32)
+    if dups:
+        seeds[:, 0], seeds[:, 1] = 5, 1000
+    knn = kernels.seed_knn(_t(f, gpu_device), _t(seeds, gpu_device, torch.int32), k).cpu().numpy()
+    for b in range(B):
+        ref = O.knn_seed_rows(f[b], seeds[b].astype(np.int64), k)
+        assert_knn_equivalent(knn[b], ref, f[b], seeds[b])
+        if dups:
+            assert list(knn[b][0]) == list(ref[0]) and list(knn[b][1]) == list(ref[1])

@@ -95,3 +95,13 @@ def test_module_refuses_cpu_and_training():
     data["testing"] = True
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m(data)
+
+
+def test_query_functions_reject_bad_precision():
+    lib = _lib.load()
+    a, b = ctypes.c_int32(), ctypes.c_int32()
+    assert lib.pdsc_attention_layout(4, 1000, 0, ctypes.byref(a), ctypes.byref(b)) == 0
+    assert lib.pdsc_encoder_plan(4, 1000, 1, ctypes.byref(a)) == 0
+    assert lib.pdsc_attention_layout(4, 1000, 7, ctypes.byref(a), ctypes.byref(b)) == 1
+    assert b"precision" in lib.pdsc_last_error()
+    assert lib.pdsc_encoder_plan(4, 1000, -1, ctypes.byref(a)) == 1
