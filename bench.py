@@ -20,6 +20,7 @@ stream the kernels run on:
   stages        -- per-stage ms of the headline forward (pdsc_forward_timing events)
   roofline_sm   -- SURVEY 8(f) row 3: the SM baseline's matrix-vector product at N=5000, HBM bound
   single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph
+  ragged        -- one call over P pairs of mixed N (0.7-1.3 N), the evaluation loop's shape
 Each roofline's `traffic` is the HBM bytes per launch of the same kernel at the
 same launch shape from the committed rocprofv3 profile (profiles/traffic_current.json).
   cpu_baseline  -- the CPU oracle (oracle/, numpy + C) on a bounded sample
@@ -476,6 +477,23 @@ def main():
                   "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1)}
         del plan1
 
+        # ---- a ragged batch (pdsc_forward_testing_ragged): P pairs of N_b ~ U[0.7 N, 1.3 N],
+        # the evaluation loop's mixed sizes in one call (datasets/ThreeDMatch.py:268-290)
+        rng = np.random.RandomState(11 + rank)
+        rsizes = rng.randint(int(0.7 * N), int(1.3 * N) + 1, size=P).tolist()
+        rps = [synthetic_pair(n, 2000 * 100003 + i, args.preset) for i, n in enumerate(rsizes)]
+        rN = max(rsizes)
+        rcorr, rsrc, rtgt = (torch.zeros((P, rN, w), dtype=torch.float32, device=dev) for w in (6, 3, 3))
+        for i, q in enumerate(rps):
+            n = rsizes[i]
+            rcorr[i, :n], rsrc[i, :n], rtgt[i, :n] = (torch.from_numpy(q[k]).to(dev)
+                                                      for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+        r_ms = event_time(lambda: kernels.forward_ragged(cfg, packed, rcorr, rsrc, rtgt, rsizes), 5, stream)
+        ragged = {"pairs": P, "num_corr_range": [int(0.7 * N), int(1.3 * N)], "padded_N": rN,
+                  "correspondences": int(sum(rsizes)), "ms_per_call": round(r_ms, 4),
+                  "correspondences_per_s": round(sum(rsizes) / (r_ms * 1e-3), 1)}
+        del rcorr, rsrc, rtgt
+
         # ---- the exact-fp32 mode (pdsc_config.precision = f32: fp32 MFMA 32x32x2 contractions)
         # on the same resident batch: its rate, and its agreement with the headline (3xf16) path
         exact = None
@@ -557,7 +575,7 @@ def main():
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
-            "stages_ms": stages, "single_pair": single, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
+            "stages_ms": stages, "single_pair": single, "ragged": ragged, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(result), flush=True)
     if grp:

@@ -352,6 +352,25 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
                                    float *final_trans, float *final_labels, const pdsc_forward_debug *debug,
                                    void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
 
+/* ---------------------------------------------- ragged testing forward -----
+ * B pairs of DIFFERENT sizes in one call: the evaluation loop's pairs
+ * (datasets/ThreeDMatch.py:268-290 keeps every keypoint, so N varies per pair;
+ * evaluation/test_3DMatch.py:33-53 runs them one by one at bs = 1).  Each pair
+ * b occupies the first counts[b] rows of N-row buffers (corr_pos [B,N,in_dim],
+ * src/tgt [B,N,3]; rows past counts[b] are ignored), and the result equals B
+ * separate bs = 1 forwards: final_trans [B,4,4]; final_labels [B,N] with rows
+ * past counts[b] set to 0.  counts: HOST int32 [B] (passed to the device as
+ * kernel arguments, no copy on the stream), each with min(cfg->k, count - 1)
+ * = min(cfg->k, N - 1) (every pair keeps the batch's k) and int(count *
+ * ratio) >= 1.  debug: as pdsc_forward_testing_debug (may be NULL), with the
+ * batch's strides S = int(N * ratio) and k; entries past a pair's own seeds are
+ * unspecified.  Workspace: pdsc_forward_workspace_bytes(cfg, B, N).           */
+int32_t pdsc_forward_testing_ragged(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                    const float *src, const float *tgt, int32_t B, int32_t N,
+                                    const int32_t *counts, float *final_trans, float *final_labels,
+                                    const pdsc_forward_debug *debug, void *workspace, size_t workspace_bytes,
+                                    pdsc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

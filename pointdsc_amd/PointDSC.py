@@ -142,6 +142,23 @@ class PointDSC(nn.Module):
         trans, labels = kernels.forward_testing(self.pdsc_config(), self.packed_weights(), corr_pos, src, tgt)
         return {"final_trans": trans, "final_labels": labels, "M": None}
 
+    def forward_list(self, datas):
+        """A list of testing inputs of DIFFERENT sizes -- the evaluation loop's
+        pairs (datasets/ThreeDMatch.py:268-290 keeps every keypoint, so N varies;
+        evaluation/test_3DMatch.py:33-53 runs them at bs = 1) -- in ONE batched
+        call (pdsc_forward_testing_ragged).  Each element is a ``forward`` input
+        dict (tensors [1,n,.] or [n,.]; the 'testing' key is implied); returns one
+        ``forward`` result dict per element: final_trans [1,4,4], final_labels
+        [1,n], M None -- equal to calling ``forward`` on each."""
+        if not datas:
+            return []
+        corr, counts = kernels.pad_pairs([d["corr_pos"] for d in datas])
+        src, _ = kernels.pad_pairs([d["src_keypts"] for d in datas])
+        tgt, _ = kernels.pad_pairs([d["tgt_keypts"] for d in datas])
+        trans, labels = kernels.forward_ragged(self.pdsc_config(), self.packed_weights(), corr, src, tgt, counts)
+        return [{"final_trans": trans[b:b + 1], "final_labels": labels[b:b + 1, :n], "M": None}
+                for b, n in enumerate(counts)]
+
     def forward_batched(self, corr_pos, src_keypts, tgt_keypts):
         """B independent pairs in one call (same N): (final_trans [B,4,4], final_labels [B,N]).
         Equivalent to B calls of ``forward`` with bs = 1."""

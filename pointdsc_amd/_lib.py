@@ -100,6 +100,8 @@ _PROTOS = {
                                        c_size_t, vp]),
     "pdsc_forward_testing_debug": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp,
                                              ctypes.POINTER(PdscForwardDebug), vp, c_size_t, vp]),
+    "pdsc_forward_testing_ragged": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, ctypes.POINTER(c_int32), vp, vp,
+                                              ctypes.POINTER(PdscForwardDebug), vp, c_size_t, vp]),
     "pdsc_ply_read_xyz": (c_int32, [ctypes.c_char_p, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "pdsc_radius_knn_workspace_bytes": (c_size_t, [c_int32]),
     "pdsc_radius_knn": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, vp, c_size_t, vp]),

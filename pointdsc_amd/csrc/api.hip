@@ -132,8 +132,8 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
 
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
                 bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
-                _Float16 *normed_s, float *conf, hipStream_t s) {
-    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s));
+                _Float16 *normed_s, float *conf, hipStream_t s, Ragged rg = {}) {
+    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg));
     if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
         float *vx = e.vexp, *vx2 = e.vexp2;
@@ -141,7 +141,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
             const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
             if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
             HIPCHK(launch_attn_pw2(packed, lay, l, q, k, v, vx, M, m_packed, d.B, d.N, d.Npad, e.feat, q2, k2, v2, vx2,
-                                   s));
+                                   s, rg));
             if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
             std::swap(q, q2);
             std::swap(k, k2);
@@ -149,14 +149,14 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
             std::swap(vx, vx2);
         }
         HIPCHK(launch_attn_pw2_last(packed, lay, q, k, v, vx, M, m_packed, d.B, d.N, d.Npad, e.feat, feat_out, normed,
-                                    normed_s, conf, s));
+                                    normed_s, conf, s, rg));
         return PDSC_OK;
     }
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
         HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
-                                s));
+                                s, rg));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         if (l + 1 < lay.L)
             HIPCHK(launch_pw_mid(packed, lay, l, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
@@ -187,15 +187,15 @@ NsmBufs carve_nsm(Carve &c, int B, int N, int S, int k, int T, bool own_split) {
 // f32: the Gram reads normed itself
 int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float *src, const float *tgt,
             const int *knn, int B, int N, int S, int k, int T, const float *sigma, const float *sigma_d,
-            const NsmBufs &nb, float *weights, int *iters, bool batch_global, hipStream_t s) {
+            const NsmBufs &nb, float *weights, int *iters, bool batch_global, hipStream_t s, Ragged rg = {}) {
     if (!f32 && !normed_s) {
         HIPCHK(launch_split_rows(normed, (size_t)B * N, nb.ns, s));
         normed_s = nb.ns;
     }
     const void *feats = f32 ? static_cast<const void *>(normed) : static_cast<const void *>(normed_s);
     if (T > 0)
-        HIPCHK(launch_nsm_seed(feats, f32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s));
-    HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, batch_global, weights, iters, s));
+        HIPCHK(launch_nsm_seed(feats, f32, src, tgt, knn, B, N, S, k, T, sigma, sigma_d, nb.hist, nb.mask, s, rg));
+    HIPCHK(launch_nsm_finish(nb.hist, nb.mask, B, S, k, T, batch_global, weights, iters, s, rg));
     return PDSC_OK;
 }
 
@@ -203,6 +203,7 @@ struct FwdBufs {
     float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights, *hsums;
     _Float16 *normed_s;
     int *seeds, *knn, *counts;
+    int *nv, *sv;  // ragged batches: per-pair correspondences and seeds
     EncBufs enc;
     NsmBufs nsm;
 };
@@ -224,6 +225,8 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.seed_trans = c.take<float>((size_t)d.B * d.S * 16);
     f.counts = c.take<int>((size_t)d.B * d.S);
     f.hsums = c.take<float>((size_t)d.B * d.S * 15);
+    f.nv = c.take<int>((size_t)d.B);
+    f.sv = c.take<int>((size_t)d.B);
     return f;
 }
 
@@ -470,22 +473,21 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
 }
 
 // -------------------------------------------------------------------- a6
-// a6 (:250-252) for the forwards: knn [B][S][k]; dist [B][S][N] and redo [B][S] scratch
+// a6 (:250-252) for the forwards: knn [B][S][k]; dist [B][S][N] scratch
 int run_seed_knn(const float *normed, const _Float16 *normed_s, bool f32, const int *seeds, int B, int N, int S,
-                 int k, float *dist, int *redo, int *knn, hipStream_t s) {
+                 int k, float *dist, int *knn, hipStream_t s, Ragged rg = {}) {
     HIPCHK(hipMemsetAsync(knn, 0, sizeof(int) * B * S * k, s));
     if (f32) {
-        HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s));
+        HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s, rg));
     } else {
-        HIPCHK(launch_knn_dist(normed_s, seeds, B, N, S, dist, s));
+        HIPCHK(launch_knn_dist(normed_s, seeds, B, N, S, dist, s, rg));
     }
-    HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s));
+    HIPCHK(launch_knn_select(dist, B, N, S, k, knn, s, rg));
     return PDSC_OK;
 }
 
 size_t pdsc_seed_knn_workspace_bytes(int32_t B, int32_t N, int32_t S) {
-    return align_bytes((size_t)B * S * N * sizeof(float)) + align_bytes((size_t)B * N * 2 * CH * sizeof(_Float16)) +
-           align_bytes((size_t)B * S * sizeof(int));
+    return align_bytes((size_t)B * S * N * sizeof(float)) + align_bytes((size_t)B * N * 2 * CH * sizeof(_Float16));
 }
 
 int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int32_t N, int32_t C,
@@ -501,10 +503,9 @@ int32_t pdsc_seed_knn(const float *normed, const int32_t *seeds, int32_t B, int3
     Carve c(ws);
     float *dist = c.take<float>((size_t)B * S * N);
     _Float16 *ns = c.take<_Float16>((size_t)B * N * 2 * CH);
-    int *redo = c.take<int>((size_t)B * S);
     const bool f32 = precision == PDSC_PRECISION_F32;
     if (!f32) HIPCHK(launch_split_rows(normed, (size_t)B * N, ns, s));
-    return run_seed_knn(normed, ns, f32, seeds, B, N, S, k, dist, redo, knn, s);
+    return run_seed_knn(normed, ns, f32, seeds, B, N, S, k, dist, knn, s);
 }
 
 // ----------------------------------------------------------------- a7-a8
@@ -596,10 +597,12 @@ int32_t pdsc_forward_testing(const pdsc_config *cfg, const float *packed, const 
                                       ws_bytes, stream);
 }
 
-int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, const float *corr_pos,
-                                   const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
-                                   float *final_labels, const pdsc_forward_debug *dbg, void *ws, size_t ws_bytes,
-                                   pdsc_stream_t stream) {
+// The testing forward of B pairs; counts (HOST, may be NULL) makes it ragged:
+// pair b uses the first counts[b] rows of its N-row buffers.
+static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                    const float *src, const float *tgt, int32_t B, int32_t N, const int32_t *counts,
+                                    float *final_trans, float *final_labels, const pdsc_forward_debug *dbg, void *ws,
+                                    size_t ws_bytes, pdsc_stream_t stream) {
     const pdsc_forward_debug no{};
     if (!dbg) dbg = &no;
     RET_IF(check_cfg(cfg));
@@ -607,10 +610,24 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
     RET_IF(make_dims(cfg, B, N, d));
     if (!packed || !corr_pos || !src || !tgt || !final_trans || !final_labels || !ws)
         return fail(PDSC_ERR_ARG, "null pointer");
+    if (counts)
+        for (int b = 0; b < B; ++b) {
+            // every pair must keep the batch's k = min(cfg k, N - 1) and have >= 1 seed
+            const int n = counts[b];
+            if (n < 2 || n > N || std::min(cfg->k, n - 1) != d.k || (int)((double)n * cfg->ratio) < 1)
+                return fail(PDSC_ERR_ARG, "counts[%d] = %d: need k + 1 = %d <= count <= N = %d and int(count * ratio) >= 1",
+                            b, n, d.k + 1, N);
+        }
     RET_IF(need_ws(ws_bytes, pdsc_forward_workspace_bytes(cfg, B, N)));
     hipStream_t s = S_(stream);
     Carve c(ws);
     const FwdBufs f = carve_forward(c, d);
+    Ragged rg;
+    if (counts) {
+        HIPCHK(launch_ragged_setup(counts, B, cfg->ratio, f.nv, f.sv, s));
+        rg.nv = f.nv;
+        rg.sv = f.sv;
+    }
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
     const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
     const bool timed = g_fcap > 0 && g_fcount && *g_fcount + PDSC_FORWARD_STAGES + 1 <= g_fcap;
@@ -622,36 +639,35 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
     // a1 (:150-153)
     const bool mpacked = !dense_m_requested() && !d.f32;  // the exact-fp32 attention reads dense M
     if (mpacked)
-        HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
+        HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     else
-        HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
+        HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s, rg));
     STAGE(2);
     // a5 (:174)
-    HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s));
-    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
+    HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s, rg));
+    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s, rg));
     STAGE(3);
     // a6 (:250-252)
-    // (f.counts: the hypotheses' inlier counts later, the overflow flags here)
-    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
+    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.knn, s, rg));
     STAGE(4);
     // a7-a8 (:257-282)
     // per pair: each pair is its own bs = 1 forward, whose allclose spans its S seeds
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
-                   nullptr, false, s));
+                   nullptr, false, s, rg));
     STAGE(5);
     // a9-a10 (:287-335)
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
-                             f.seed_trans, f.counts, f.hsums, s));
+                             f.seed_trans, f.counts, f.hsums, s, rg));
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
-                              nullptr, nullptr, final_trans, final_labels, s));
+                              nullptr, nullptr, final_trans, final_labels, s, rg));
     if (dbg->trans_pre_refine)
         HIPCHK(hipMemcpyAsync(dbg->trans_pre_refine, final_trans, sizeof(float) * 16 * d.B, hipMemcpyDeviceToDevice, s));
     STAGE(6);
     // a11 (:186, :403-438)
-    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s));
+    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s, rg));
     STAGE(7);
 #undef STAGE
     if (dbg->conf) HIPCHK(hipMemcpyAsync(dbg->conf, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
@@ -660,6 +676,23 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
     if (dbg->weights)
         HIPCHK(hipMemcpyAsync(dbg->weights, f.weights, sizeof(float) * d.B * d.S * d.k, hipMemcpyDeviceToDevice, s));
     return PDSC_OK;
+}
+
+int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                   const float *src, const float *tgt, int32_t B, int32_t N, float *final_trans,
+                                   float *final_labels, const pdsc_forward_debug *dbg, void *ws, size_t ws_bytes,
+                                   pdsc_stream_t stream) {
+    return forward_testing_impl(cfg, packed, corr_pos, src, tgt, B, N, nullptr, final_trans, final_labels, dbg, ws,
+                                ws_bytes, stream);
+}
+
+int32_t pdsc_forward_testing_ragged(const pdsc_config *cfg, const float *packed, const float *corr_pos,
+                                    const float *src, const float *tgt, int32_t B, int32_t N, const int32_t *counts,
+                                    float *final_trans, float *final_labels, const pdsc_forward_debug *dbg, void *ws,
+                                    size_t ws_bytes, pdsc_stream_t stream) {
+    if (!counts) return fail(PDSC_ERR_ARG, "counts is NULL");
+    return forward_testing_impl(cfg, packed, corr_pos, src, tgt, B, N, counts, final_trans, final_labels, dbg, ws,
+                                ws_bytes, stream);
 }
 
 
@@ -698,7 +731,7 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s));
     // a6-a10 as in testing (:182 -> cal_seed_trans), no post-refinement (:185-186)
     // (f.counts: the hypotheses' inlier counts later, the overflow flags here)
-    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.counts, f.knn, s));
+    RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.knn, s));
     // the training batch is ONE reference forward: torch.allclose over all B * S seeds (:354)
     RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm,
                    f.weights, nullptr, true, s));

@@ -42,12 +42,15 @@ PDSC_DEV f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
 
 struct AttnGrid {
     int B, N, Npad, nqb, nsplit, sps;  // sps = stages per split
+    const int *nv;  // ragged batches: pair b's correspondences (N, Npad: the strides), or null
+    PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
 // Host: split-K factor so that the grid fills the chip (~`target` workgroups).
 template <int NW, int KTS>
 inline AttnGrid attention_grid(int B, int N, int target) {
     AttnGrid g;
+    g.nv = nullptr;
     g.B = B;
     g.N = N;
     g.Npad = round_up(N, QB);
@@ -95,7 +98,9 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
 
     int b, qb, split;
     attention_block_coords(g, XCD, b, qb, split);
-    const int N = g.N, Npad = g.Npad;
+    // N: this pair's keys (a ragged batch's pairs differ); Ns, Npad: the batch's strides
+    const int N = g.n(b), Ns = g.N, Npad = g.Npad;
+    if (qb * (NW * 32) >= N) return;  // past a ragged pair's end (workgroup-uniform)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
     const int q0 = qb * (NW * 32) + wave * 32;
     const int nst = (N + KTS - 1) / KTS;
@@ -105,7 +110,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
     const __amdgpu_buffer_rsrc_t rV = make_rsrc(v + pbase, (uint32_t)Npad * CH * 4);
     // M of this pair (N <= 32767 so the byte range fits the 32-bit descriptor);
     // rows >= N read 0 through the range check (and are masked to -inf below)
-    const __amdgpu_buffer_rsrc_t rM = make_rsrc(M + (size_t)b * N * N, (uint32_t)N * (uint32_t)N * 4u);
+    const __amdgpu_buffer_rsrc_t rM = make_rsrc(M + (size_t)b * Ns * Ns, (uint32_t)Ns * (uint32_t)Ns * 4u);
     const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
     const int qq = q0 + l32;
     const bool active = q0 < Npad;  // waves past the padded end (NW*32 > 128 granularity)
@@ -169,12 +174,12 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
     float m_run = -INFINITY, l_run = 0.0f;
     // FASTEXP: logits in log2 units (log2(e)/sqrt(128)); else natural units (1/sqrt(128))
     const float scale = FASTEXP ? 0.12751743082459868f : 0.08838834764831845f;
-    const uint32_t Nb = (uint32_t)N * 4;
+    const uint32_t Nb = (uint32_t)Ns * 4;
 
     auto subtile = [&](const float *Kl, const float *Vl, int key0) {
         // M[key][q] for this lane's 16 keys (rows acc_row(r, h)) -- issued before the MFMAs
         float mv[16];
-        const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
+        const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)Ns + (uint32_t)qq) * 4;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const uint32_t o = vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * Nb;
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 ? 2 : 1)) void attention_kernel_t
                 mv[r] = buf_ld(rM, o, 0);
             } else {
                 const int key = key0 + acc_row(r, h);
-                mv[r] = key < N ? *reinterpret_cast<const float *>(reinterpret_cast<const char *>(M + (size_t)b * N * N) + o) : 0.0f;
+                mv[r] = key < N ? *reinterpret_cast<const float *>(reinterpret_cast<const char *>(M + (size_t)b * Ns * Ns) + o) : 0.0f;
             }
         }
         f32x16 S = zero16();

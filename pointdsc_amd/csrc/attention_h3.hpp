@@ -203,11 +203,15 @@ PDSC_DEV __amdgpu_buffer_rsrc_t h3_rsrc(const void *base, uint32_t bytes) {
 
 struct AttnGridH3 {
     int B, N, Npad, nqb, nsplit, sps;  // sps = 32-key tiles per split
+    // ragged batches: pair b's correspondences (N, Npad: the batch's strides), or null
+    const int *nv;
+    PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
 template <int NW>
 inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
     AttnGridH3 g;
+    g.nv = nullptr;
     g.B = B;
     g.N = N;
     g.Npad = round_up(N, QB);
@@ -249,7 +253,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
                                 const float *__restrict__ M, const AttnGridH3 &g, const AttnBlock &blk, char *h3smem,
                                 int wave, int lane, f32x16 (&O)[4], float &m_run, float &l_run) {
     const int b = blk.b, qb = blk.qb, split = blk.split;
-    const int N = g.N, Npad = g.Npad;
+    const int N = g.n(b), Npad = g.Npad;  // this pair's keys; the batch's row stride
     const int h = lane >> 5, l32 = lane & 31;
     const int q0 = qb * (NW * 32) + wave * 32;
     const int nst = (N + H3_TILE - 1) / H3_TILE;
@@ -259,8 +263,8 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
 
     const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
     const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
-    const int mnt = mpack_ntile(N);
-    const size_t mper = PACKED ? (size_t)mnt * (mnt + 1) / 2 * MPACK_T * MPACK_T : (size_t)N * N;
+    const int mnt = mpack_ntile(g.N);  // M's layout is the batch stride's
+    const size_t mper = PACKED ? (size_t)mnt * (mnt + 1) / 2 * MPACK_T * MPACK_T : (size_t)g.N * g.N;
     const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M + (size_t)b * mper, (uint32_t)(mper * 4u));
 
     // this lane's query: 8 k-steps x (hi, lo) fragments (16 coalesced 1-KiB loads)
@@ -293,7 +297,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     m_run = -INFINITY;
     l_run = 0.0f;
     const float scale = 0.12751743082459868f;  // log2(e) / sqrt(128)
-    const uint32_t Nb = (uint32_t)N * 4;
+    const uint32_t Nb = (uint32_t)g.N * 4;
 
     const float *vexp_b = vexp + (size_t)b * (Npad / H3_TILE);
     const __amdgpu_buffer_rsrc_t rE = h3_rsrc(vexp_b, (uint32_t)(Npad / H3_TILE) * 4u);
@@ -326,7 +330,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
                 }
             }
         } else {
-            const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)N + (uint32_t)qq) * 4;
+            const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)g.N + (uint32_t)qq) * 4;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 mv[r] = __builtin_bit_cast(
@@ -461,6 +465,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     float *__restrict__ ml) {
     extern __shared__ __attribute__((aligned(16))) char h3smem[];
     const AttnBlock blk = attention_h3_block(g, XCD);
+    if (blk.qb * (NW * 32) >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
     const int b = blk.b, split = blk.split, Npad = g.Npad;
     // wave in an SGPR: every wave-uniform branch (M orientation, active, the
     // barrier's count) is then a scalar branch, never an exec-masked one

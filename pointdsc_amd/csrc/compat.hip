@@ -11,6 +11,8 @@
 // two correctly-rounded sqrtf and one correctly-rounded division (~40 VALU
 // ops), so computing each pair once halves the VALU work that would otherwise
 // sit right at the write roofline.  Stores are 16 B per lane.
+#include <algorithm>
+
 #include "pdsc_internal.hpp"
 
 namespace pdsc {
@@ -76,9 +78,9 @@ PDSC_DEV void compat4(const float xs[4], const float xt[4], float s2, float rs2,
 }
 
 __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ src,
-                                                     const float *__restrict__ tgt, int N,
+                                                     const float *__restrict__ tgt, int Nstr,
                                                      int ntile, const float *__restrict__ sigma_d_ptr,
-                                                     float *__restrict__ M) {
+                                                     float *__restrict__ M, Ragged rg) {
     __shared__ float tileT[CT][CT + 1];
     __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
     // linear upper-triangular tile index -> (ti, tj), ti <= tj
@@ -86,15 +88,19 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
     while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
     const int tj = ti + t;
     const int b = blockIdx.y;
+    // N: this pair's correspondences (rows / columns past it are not written);
+    // Nstr: the row stride of the batch's buffers
+    const int N = rg.n(b, Nstr);
+    if (tj * CT >= N) return;  // workgroup-uniform
     const float sd = sigma_d_ptr[0];
     const float s2 = sd * sd;
     const float rs2 = 1.0f / s2;  // correctly rounded (the library division)
     // fast path: every squared distance of the tile is 0 or >= 2^-96 and s2 is a normal
     // number with a normal reciprocal (checked per element below, wave-uniformly)
     const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
-    src += (size_t)b * N * 3;
-    tgt += (size_t)b * N * 3;
-    M += (size_t)b * N * N;
+    src += (size_t)b * Nstr * 3;
+    tgt += (size_t)b * Nstr * 3;
+    M += (size_t)b * Nstr * Nstr;
     const int tid = threadIdx.x;
     const int i0 = ti * CT, j0 = tj * CT;
     for (int e = tid; e < CT * 3; e += 256) {
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
     __syncthreads();
     // thread -> 4 consecutive columns (cq*4..+3) of 4 rows (rq, rq+16, rq+32, rq+48)
     const int cq = tid & 15, rq = tid >> 4;
-    const bool vec = (N & 3) == 0;
+    const bool vec = (Nstr & 3) == 0;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
         const int r = rq + 16 * rr;
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
         for (int q = 0; q < 4; ++q) tileT[cq * 4 + q][r] = out[q];
         if (i < N) {
             const int j = j0 + cq * 4;
-            float *dst = M + (size_t)i * N + j;
+            float *dst = M + (size_t)i * Nstr + j;
             if (vec && j + 3 < N) {
                 *reinterpret_cast<f32x4 *>(dst) = f32x4{out[0], out[1], out[2], out[3]};
             } else {
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
         const int i = j0 + r;
         if (i >= N) continue;
         const int j = i0 + cq * 4;
-        float *dst = M + (size_t)i * N + j;
+        float *dst = M + (size_t)i * Nstr + j;
         const float o0 = tileT[r][cq * 4], o1 = tileT[r][cq * 4 + 1], o2 = tileT[r][cq * 4 + 2],
                     o3 = tileT[r][cq * 4 + 3];
         if (vec && j + 3 < N) {
@@ -183,24 +189,30 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
 // segments strided by 4N B: ~2.9 TB/s at N = 5000 against ~5.3 TB/s for
 // contiguous stores, tools/compat_bench.hip.)  Entries past N are written as 0.
 __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restrict__ src,
-                                                            const float *__restrict__ tgt, int N, int ntile,
+                                                            const float *__restrict__ tgt, int Nstr, int ntile,
                                                             const float *__restrict__ sigma_d_ptr,
-                                                            float *__restrict__ Mp) {
+                                                            float *__restrict__ Mp, Ragged rg) {
     __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
     __shared__ CompatScratch scr[4];
     int t = blockIdx.x, ti = 0;
     while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
     const int tj = ti + t;
     const int b = blockIdx.y;
+    // N: this pair's correspondences; Nstr: the batch's stride (the packed layout
+    // is that of Nstr for every pair).  Blocks whose rows all lie past N are
+    // never read: every tile an attention wave of this pair reads has its
+    // smaller tile index below ceil(N / 32).
+    const int N = rg.n(b, Nstr);
+    if (ti * CT >= N) return;  // workgroup-uniform
     const float sd = sigma_d_ptr[0];
     const float s2 = sd * sd;
     const float rs2 = 1.0f / s2;
     const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
     const float kzero = 2.0f * s2 * (1.0f + 0x1p-10f), gmax = 0x1p20f * s2;  // compat4's zero test
-    src += (size_t)b * N * 3;
-    tgt += (size_t)b * N * 3;
-    const int nt32 = mpack_ntile(N);
-    float *Mb = Mp + (size_t)b * mpack_floats(N);
+    src += (size_t)b * Nstr * 3;
+    tgt += (size_t)b * Nstr * 3;
+    const int nt32 = mpack_ntile(Nstr);
+    float *Mb = Mp + (size_t)b * mpack_floats(Nstr);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int i0 = ti * CT, j0 = tj * CT;
     for (int e = tid; e < CT * 3; e += 256) {
@@ -248,20 +260,42 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
 }
 
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
-                                float *Mp, hipStream_t stream) {
+                                float *Mp, hipStream_t stream, Ragged rg) {
     const int ntile = (N + CT - 1) / CT;  // 64-point compute blocks
     const int ntri = ntile * (ntile + 1) / 2;
-    hipLaunchKernelGGL(compat_packed_kernel, dim3(ntri, B), dim3(256), 0, stream, src, tgt, N, ntile, sigma_d, Mp);
+    hipLaunchKernelGGL(compat_packed_kernel, dim3(ntri, B), dim3(256), 0, stream, src, tgt, N, ntile, sigma_d, Mp, rg);
     return hipGetLastError();
 }
 
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
-                         float *M, hipStream_t stream) {
+                         float *M, hipStream_t stream, Ragged rg) {
     const int ntile = (N + CT - 1) / CT;
     const int ntri = ntile * (ntile + 1) / 2;
     hipLaunchKernelGGL(compat_kernel, dim3(ntri, B), dim3(256), 0, stream, src, tgt, N, ntile,
-                       sigma_d, M);
+                       sigma_d, M, rg);
     return hipGetLastError();
+}
+
+// counts -> nv, sv (one launch per RAGGED_CHUNK pairs, the counts as a kernel argument)
+struct RaggedChunk {
+    int32_t n[RAGGED_CHUNK];
+};
+__global__ void ragged_setup_kernel(RaggedChunk c, int nb, double ratio, int *__restrict__ nv, int *__restrict__ sv) {
+    const int i = threadIdx.x;
+    if (i >= nb) return;
+    nv[i] = c.n[i];
+    sv[i] = (int)((double)c.n[i] * ratio);  // int(num_corr * self.ratio) (models/PointDSC.py:174)
+}
+
+hipError_t launch_ragged_setup(const int32_t *counts, int B, double ratio, int *nv, int *sv, hipStream_t s) {
+    for (int b0 = 0; b0 < B; b0 += RAGGED_CHUNK) {
+        RaggedChunk c{};
+        const int nb = std::min(RAGGED_CHUNK, B - b0);
+        for (int i = 0; i < nb; ++i) c.n[i] = counts[b0 + i];
+        hipLaunchKernelGGL(ragged_setup_kernel, dim3(1), dim3(RAGGED_CHUNK), 0, s, c, nb, ratio, nv + b0, sv + b0);
+        HIP_RET(hipGetLastError());
+    }
+    return hipSuccess;
 }
 
 }  // namespace pdsc

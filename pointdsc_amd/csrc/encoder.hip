@@ -148,9 +148,10 @@ int attention_nsplit(int B, int N, bool f32) { return f32 ? f32_grid(B, N).nspli
 
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
-                            hipStream_t s) {
+                            hipStream_t s, Ragged rg) {
     if (f32) {  // fp32 [B][Npad][CH] rows, dense M
-        const AttnGrid g = f32_grid(B, N);
+        AttnGrid g = f32_grid(B, N);
+        g.nv = rg.nv;
         if (m_packed || g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
         const size_t lds = attention_lds_bytes<ATT_NW, ATT_F32_KTS>();
         hipLaunchKernelGGL((attention_kernel_t<ATT_NW, ATT_F32_KTS, false, true>), dim3(g.B * g.nqb * g.nsplit),
@@ -161,7 +162,8 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     }
     const _Float16 *qs = static_cast<const _Float16 *>(q), *ks = static_cast<const _Float16 *>(k),
                    *vs = static_cast<const _Float16 *>(v);
-    const AttnGridH3 g = prod_grid(B, N);
+    AttnGridH3 g = prod_grid(B, N);
+    g.nv = rg.nv;
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     if (m_packed)
         hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), dim3(g.B * g.nqb * g.nsplit),
@@ -569,15 +571,17 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
                                                        const float *__restrict__ corr, int in_dim,
                                                        int N, int Npad, float *__restrict__ feat,
                                                        _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                                                       _Float16 *__restrict__ V, float *__restrict__ vexp) {
+                                                       _Float16 *__restrict__ V, float *__restrict__ vexp,
+                                                       const int *__restrict__ nv) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PTT * S132, *cp = XB;  // cp: [PTT][in_dim], consumed before XB is written
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
+    const int n = nv ? nv[b] : N;  // this pair's rows (ragged batches); N: the row stride
     for (int e = tid; e < PTT * in_dim; e += 256) {
         const int p = e / in_dim;
-        cp[e] = (p0 + p < N) ? corr[((size_t)b * N + p0) * in_dim + e] : 0.0f;
+        cp[e] = (p0 + p < n) ? corr[((size_t)b * N + p0) * in_dim + e] : 0.0f;
     }
     // thread -> output channel j (both halves of the block cover rows of opposite parity)
     const int j = tid & (CH - 1), p_off = tid >> 7;
@@ -1109,14 +1113,16 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_first_kernel(const fl
                                                                  size_t l0b, PwDense4 d, const float *__restrict__ corr,
                                                                  int in_dim, int N, int Npad, float *__restrict__ featL,
                                                                  _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                                                                 _Float16 *__restrict__ V, float *__restrict__ vexp) {
+                                                                 _Float16 *__restrict__ V, float *__restrict__ vexp,
+                                                                 const int *__restrict__ nv) {
     PW2_PROLOGUE
     const int l32 = lane & 31;
+    const int n = nv ? nv[b] : N;  // this pair's rows (ragged batches); N: the row stride
     w2_coef_qkv(cf, pk, d, tid);
     f16x8 xh[8], xl[8];
     if (active) {
-        const float *cp = corr + ((size_t)b * N + min(row, N - 1)) * in_dim;
-        const bool in = row < N;
+        const float *cp = corr + ((size_t)b * N + min(row, n - 1)) * in_dim;
+        const bool in = row < n;
         f32x16 acc[4] = {zero16(), zero16(), zero16(), zero16()};
         for (int j = 0; j < (in_dim + 1) / 2; ++j) {
             const int i = 2 * j + h;
@@ -1175,6 +1181,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     _Float16 *__restrict__ V, float *__restrict__ vexp) {
     extern __shared__ __attribute__((aligned(16))) char w2smem[];
     const AttnBlock blk = attention_h3_block(g, true);
+    if (blk.qb * PW2_PTS >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
     const int b = blk.b, Npad = g.Npad, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
               lane = tid & 63;
     const int row = blk.qb * PW2_PTS + wave * 32 + (lane & 31);
@@ -1315,6 +1322,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_last_kernel(
     float *__restrict__ conf) {
     extern __shared__ __attribute__((aligned(16))) char w2smem[];
     const AttnBlock blk = attention_h3_block(g, true);
+    if (blk.qb * PW2_PTS >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
     const int b = blk.b, N = g.N, Npad = g.Npad, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6),
               lane = tid & 63;
     const int row = blk.qb * PW2_PTS + wave * 32 + (lane & 31);
@@ -1378,8 +1386,9 @@ bool attention_fused(int B, int N, bool f32) {
 
 hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
                            const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
-                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s) {
-    const AttnGridH3 g = fused_grid(B, N);
+                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s, Ragged rg) {
+    AttnGridH3 g = fused_grid(B, N);
+    g.nv = rg.nv;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
     const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
     const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
@@ -1398,8 +1407,9 @@ hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer
 hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, const void *q, const void *k,
                                 const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N,
                                 int Npad, const float *feat, float *feat_out, float *normed, _Float16 *normed_s,
-                                float *conf, hipStream_t s) {
-    const AttnGridH3 g = fused_grid(B, N);
+                                float *conf, hipStream_t s, Ragged rg) {
+    AttnGridH3 g = fused_grid(B, N);
+    g.nv = rg.nv;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad) return hipErrorInvalidValue;
     W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
     w2_sched_add(S, lay.c0, CH, CLS);
@@ -1447,18 +1457,19 @@ static bool small_tiles(int B, int Npad) {
     } while (0)
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
-                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s) {
+                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
+                           Ragged rg) {
     if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
         const W2Sched S = sched_qkv(W2Sched{}, dense4(lay.layer[0]));
         hipLaunchKernelGGL(pw2_first_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
                            packed, S, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K,
-                           V, vexp);
+                           V, vexp, rg.nv);
         return hipGetLastError();
     }
     PW_LAUNCH(pw_first_kernel, Npad, packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad,
-              feat, Q, K, V, vexp);
+              feat, Q, K, V, vexp, rg.nv);
     return hipGetLastError();
 }
 

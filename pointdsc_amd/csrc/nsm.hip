@@ -33,18 +33,22 @@ namespace pdsc {
 constexpr int KNN_KPB = 5;
 
 __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
-                                                       const int *__restrict__ seeds, int N, int S,
-                                                       float *__restrict__ dist) {
+                                                       const int *__restrict__ seeds, int Nstr, int Sstr,
+                                                       float *__restrict__ dist, Ragged rg) {
     __shared__ f16x8 Bt[32 * 32];
     const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, l32 = lane & 31;
+    // this pair's keys and seeds; Nstr, Sstr: the batch's strides (rows [b][s] of
+    // dist are Nstr long)
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    if (blockIdx.y * 128 >= S || blockIdx.x * KNN_KPB * 32 >= N) return;  // workgroup-uniform
     const int s0 = (blockIdx.y * 4 + wave) * 32;
     const bool active = s0 < S;  // wave-uniform; every wave joins the barriers
-    const _Float16 *F = ns + (size_t)b * N * 2 * CH;
+    const _Float16 *F = ns + (size_t)b * Nstr * 2 * CH;
     const int sidx = s0 + l32;
     f16x8 ah[8], al[8];
     if (active) {
-        const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
+        const int seed = (sidx < S) ? seeds[(size_t)b * Sstr + sidx] : 0;
         const char *row = reinterpret_cast<const char *>(F + (size_t)min(max(seed, 0), N - 1) * 2 * CH);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -81,17 +85,17 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int s = s0 + acc_row(r, h);
-                if (s < S) dist[((size_t)b * S + s) * N + j] = 2.0f - 2.0f * acc[r];
+                if (s < S) dist[((size_t)b * Sstr + s) * Nstr + j] = 2.0f - 2.0f * acc[r];
             }
         }
     }
 }
 
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
-                           hipStream_t s) {
+                           hipStream_t s, Ragged rg) {
     const int nkt = (N + 31) / 32;
     hipLaunchKernelGGL(knn_dist_kernel, dim3((nkt + KNN_KPB - 1) / KNN_KPB, (S + 127) / 128, B), dim3(256), 0, s,
-                       ns, seeds, N, S, dist);
+                       ns, seeds, N, S, dist, rg);
     return hipGetLastError();
 }
 
@@ -101,15 +105,16 @@ hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, i
 // KNN_KPB key tiles, each key fragment read from L2 as 16-B pieces; k-step
 // 4j + e of lane (h, .) is channel 8j + 4h + e for both operands.
 __global__ __launch_bounds__(256) void knn_dist_f32_kernel(const float *__restrict__ normed,
-                                                           const int *__restrict__ seeds, int N, int S,
-                                                           float *__restrict__ dist) {
+                                                           const int *__restrict__ seeds, int Nstr, int Sstr,
+                                                           float *__restrict__ dist, Ragged rg) {
     const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, l32 = lane & 31;
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);  // this pair's keys and seeds
     const int s0 = (blockIdx.y * 4 + wave) * 32;
     if (s0 >= S) return;  // wave-uniform; no barriers
-    const float *F = normed + (size_t)b * N * CH;
+    const float *F = normed + (size_t)b * Nstr * CH;
     const int sidx = s0 + l32;
-    const int seed = (sidx < S) ? seeds[(size_t)b * S + sidx] : 0;
+    const int seed = (sidx < S) ? seeds[(size_t)b * Sstr + sidx] : 0;
     const float *srow = F + (size_t)min(max(seed, 0), N - 1) * CH + 4 * h;
     f32x4 a[CH / 8];
 #pragma unroll
@@ -130,17 +135,17 @@ __global__ __launch_bounds__(256) void knn_dist_f32_kernel(const float *__restri
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int sr = s0 + acc_row(r, h);
-                if (sr < S) dist[((size_t)b * S + sr) * N + j] = 2.0f - 2.0f * acc[r];
+                if (sr < S) dist[((size_t)b * Sstr + sr) * Nstr + j] = 2.0f - 2.0f * acc[r];
             }
         }
     }
 }
 
 hipError_t launch_knn_dist_f32(const float *normed, const int *seeds, int B, int N, int S, float *dist,
-                               hipStream_t s) {
+                               hipStream_t s, Ragged rg) {
     const int nkt = (N + 31) / 32;
     hipLaunchKernelGGL(knn_dist_f32_kernel, dim3((nkt + KNN_KPB - 1) / KNN_KPB, (S + 127) / 128, B), dim3(256), 0,
-                       s, normed, seeds, N, S, dist);
+                       s, normed, seeds, N, S, dist, rg);
     return hipGetLastError();
 }
 
@@ -186,8 +191,8 @@ constexpr int KNN_BINCAP = 64;
 constexpr int KNN_FASTCAP = 128;
 
 template <int R>
-__global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int N, int S,
-                                                         int k, int *__restrict__ knn, const int *__restrict__ only) {
+__global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int Nstr, int Sstr,
+                                                         int k, int *__restrict__ knn, Ragged rg) {
     __shared__ uint32_t hist[4][256];
     __shared__ uint32_t ckey[4][64];
     __shared__ int cidx[4][64];
@@ -197,9 +202,10 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     __shared__ int fidxb[4][KNN_FASTCAP];
     const int b = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s = blockIdx.x * (blockDim.x >> 6) + wave;
+    // this pair's keys and seeds; Nstr, Sstr: the batch's strides
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
-    if (only && !only[(size_t)b * S + s]) return;  // the fused kernel's overflow seeds only
-    const float *row = dist + ((size_t)b * S + s) * N;
+    const float *row = dist + ((size_t)b * Sstr + s) * Nstr;
     const uint32_t want = k + 1;
     // Fast path (no atomics): tau0 = the want-th smallest of the 64 per-lane
     // minima bounds the want-th smallest key from above (at least `want` keys are
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         // index of this lane's i-th key
         auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
         if constexpr (R > 0) {
-            const bool vec = (N & 3) == 0;  // rows 16-B aligned
+            const bool vec = (Nstr & 3) == 0;  // rows 16-B aligned
 #pragma unroll
             for (int i4 = 0; i4 < R / 4; ++i4) {
                 const int j = 256 * i4 + 4 * lane;
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 r0 += (mu < k0) || (mu == k0 && mi < i0);
                 r1 += (mu < k1) || (mu == k1 && mi < i1);
             }
-            int *out = knn + ((size_t)b * S + s) * k;
+            int *out = knn + ((size_t)b * Sstr + s) * k;
             if (e0 < (int)c && r0 > 0 && r0 < want) out[r0 - 1] = i0;  // drop position 0 (:68)
             if (e1 < (int)c && r1 > 0 && r1 < want) out[r1 - 1] = i1;
             return;
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             const uint32_t mu = ckey[wave][m];
             rank += (mu < ku) || (mu == ku && cidx[wave][m] < ki);
         }
-        if (rank > 0) knn[((size_t)b * S + s) * k + rank - 1] = ki;  // drop position 0 (:68)
+        if (rank > 0) knn[((size_t)b * Sstr + s) * k + rank - 1] = ki;  // drop position 0 (:68)
     }
 }
 
@@ -437,26 +443,26 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
 static int seed_wpb(int B, int S) { return (long)B * ((S + 3) / 4) < 512 ? 1 : 4; }
 
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s,
-                             const int *only) {
+                             Ragged rg) {
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const int R = (N + 63) / 64;
     if (R <= 16)
-        hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 32)
-        hipLaunchKernelGGL(knn_select_kernel<32>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<32>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 48)
-        hipLaunchKernelGGL(knn_select_kernel<48>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<48>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 64)
-        hipLaunchKernelGGL(knn_select_kernel<64>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<64>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 80)
-        hipLaunchKernelGGL(knn_select_kernel<80>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<80>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 96)
-        hipLaunchKernelGGL(knn_select_kernel<96>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<96>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else if (R <= 128)
-        hipLaunchKernelGGL(knn_select_kernel<128>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<128>, grid, block, 0, s, dist, N, S, k, knn, rg);
     else
-        hipLaunchKernelGGL(knn_select_kernel<0>, grid, block, 0, s, dist, N, S, k, knn, only);
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, block, 0, s, dist, N, S, k, knn, rg);
     return hipGetLastError();
 }
 
@@ -521,11 +527,12 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
                                                        const int *__restrict__ knn, int N, int S, int k, int T,
                                                        const float *__restrict__ sigma_p,
                                                        const float *__restrict__ sigma_d_p,
-                                                       float *__restrict__ hist, unsigned *__restrict__ seed_flags) {
+                                                       float *__restrict__ hist, unsigned *__restrict__ seed_flags,
+                                                       Ragged rg) {
     extern __shared__ __attribute__((aligned(16))) float nsm_sdyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.y, s = blockIdx.x * (blockDim.x >> 6) + wave;
-    if (s >= S) return;  // wave-uniform
+    if (s >= rg.s(b, S)) return;  // wave-uniform (a ragged pair's own seed count; S, N: the strides)
     const int tls = k + 1;
     float *Tl = nsm_sdyn + (size_t)wave * (k * tls + KMAX * NSM_PSTR + KMAX);
     float *P = Tl + k * tls;  // [KMAX][NSM_PSTR]: src xyz, tgt xyz
@@ -646,14 +653,14 @@ size_t nsm_seed_lds_bytes(int k, int wpb) {
 
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
                            int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
-                           unsigned *seed_flags, hipStream_t s) {
+                           unsigned *seed_flags, hipStream_t s, Ragged rg) {
     if (k < 1 || k > KMAX) return hipErrorInvalidValue;
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const size_t lds = nsm_seed_lds_bytes(k, wpb);
 #define NSM_LAUNCH(F, KC)                                                                                     \
     hipLaunchKernelGGL((nsm_seed_kernel<F, KC>), grid, block, lds, s, feats, src, tgt, knn, N, S, k, T, sigma, \
-                       sigma_d, hist, seed_flags)
+                       sigma_d, hist, seed_flags, rg)
     const int kc = (k + 15) / 16;
     if (f32) {
         if (kc == 1) NSM_LAUNCH(true, 16); else if (kc == 2) NSM_LAUNCH(true, 32);
@@ -670,12 +677,15 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
 __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict__ hist,
                                                         const unsigned *__restrict__ seed_flags, int S,
                                                         int k, int T, int batch_global, float *__restrict__ weights,
-                                                        int *__restrict__ iters_used) {
+                                                        int *__restrict__ iters_used, Ragged rg) {
     const int b = blockIdx.y, s = blockIdx.x, a = threadIdx.x;
+    const int Sb = rg.s(b, S);  // this pair's seeds (a ragged batch); S: the stride
+    if (s >= Sb) return;
     // the allclose bits ANDed over the seeds torch.allclose sees at once (:354):
     // the pair's S seeds (a bs = 1 testing forward) or, batch_global, all
     // gridDim.y * S seeds of the call (the training forward's [bs * S, k] iterate)
-    const size_t q0 = batch_global ? 0 : (size_t)b * S, nq = batch_global ? (size_t)gridDim.y * S : (size_t)S;
+    // (ragged batches run per pair: pdsc_forward_testing_ragged is B bs = 1 forwards)
+    const size_t q0 = batch_global ? 0 : (size_t)b * S, nq = batch_global ? (size_t)gridDim.y * S : (size_t)Sb;
     unsigned all = 0xffffffffu;
     if (T > 0)
         for (size_t q = a; q < nq; q += 64) all &= seed_flags[q0 + q];
@@ -692,9 +702,10 @@ __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict_
 }
 
 hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T,
-                             bool batch_global, float *weights, int *iters_used, hipStream_t s) {
+                             bool batch_global, float *weights, int *iters_used, hipStream_t s, Ragged rg) {
+    if (batch_global && rg.sv) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nsm_finish_kernel, dim3(S, B), dim3(64), 0, s, hist, seed_flags, S, k, T, (int)batch_global,
-                       weights, iters_used);
+                       weights, iters_used, rg);
     return hipGetLastError();
 }
 
@@ -711,10 +722,10 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
                                                           const float *__restrict__ tgt,
                                                           const int *__restrict__ knn,
                                                           const float *__restrict__ weights, int N,
-                                                          int S, int k, float *__restrict__ sums) {
+                                                          int S, int k, float *__restrict__ sums, Ragged rg) {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
     const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (s >= S) return;
+    if (s >= rg.s(b, S)) return;  // (N, S: the strides; knn entries lie below this pair's count)
     const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
     float w = 0, ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
     if (lane < k) {
@@ -773,10 +784,10 @@ PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[
     T[15] = 1.0f;
 }
 
-__global__ __launch_bounds__(64) void kabsch_solve_kernel(const float *__restrict__ sums, int n,
-                                                          float *__restrict__ trans) {
+__global__ __launch_bounds__(64) void kabsch_solve_kernel(const float *__restrict__ sums, int n, int S,
+                                                          float *__restrict__ trans, Ragged rg) {
     const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || i % S >= rg.s(i / S, S)) return;  // (a ragged pair's seeds end early)
     const float *p = sums + (size_t)i * HSUM;
     float H[9], cA[3], cB[3], T[16];
 #pragma unroll
@@ -794,18 +805,20 @@ __global__ __launch_bounds__(64) void kabsch_solve_kernel(const float *__restric
 __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restrict__ src,
                                                             const float *__restrict__ tgt,
                                                             const float *__restrict__ seed_trans,
-                                                            int N, int S, float tau2,
-                                                            int *__restrict__ counts) {
+                                                            int Nstr, int S, float tau2,
+                                                            int *__restrict__ counts, Ragged rg) {
     __shared__ float Ts[HS][12];
     __shared__ int wc[4][HS];
     const int b = blockIdx.y, s0 = blockIdx.x * HS, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ns = min(HS, S - s0);
+    const int N = rg.n(b, Nstr);  // this pair's correspondences; Nstr, S: the strides
+    if (s0 >= rg.s(b, S)) return;  // workgroup-uniform
+    const int ns = min(HS, rg.s(b, S) - s0);
     if (tid < HS * 12) {
         const int q = tid / 12, e = tid % 12;
         Ts[q][e] = (q < ns) ? seed_trans[((size_t)b * S + s0 + q) * 16 + e] : 0.0f;
     }
     __syncthreads();
-    const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
+    const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
     int c[HS];
 #pragma unroll
     for (int q = 0; q < HS; ++q) c[q] = 0;
@@ -826,14 +839,14 @@ __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restr
 
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             float *sums, hipStream_t s) {
+                             float *sums, hipStream_t s, Ragged rg) {
     const int wpb = seed_wpb(B, S);
     hipLaunchKernelGGL(kabsch_sums_kernel, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn, weights,
-                       N, S, k, sums);
+                       N, S, k, sums, rg);
     const int n = B * S;
-    hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, seed_trans);
+    hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, S, seed_trans, rg);
     hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
-                       seed_trans, N, S, sqrt_ge_threshold(tau), counts);
+                       seed_trans, N, S, sqrt_ge_threshold(tau), counts, rg);
     return hipGetLastError();
 }
 
@@ -841,18 +854,19 @@ hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn,
 __global__ __launch_bounds__(256) void select_best_kernel(const float *__restrict__ src,
                                                           const float *__restrict__ tgt,
                                                           const float *__restrict__ seed_trans,
-                                                          const int *__restrict__ counts, int N, int S,
+                                                          const int *__restrict__ counts, int Nstr, int Sstr,
                                                           float tau, float *__restrict__ fitness,
                                                           int *__restrict__ best_out,
                                                           float *__restrict__ trans,
-                                                          float *__restrict__ labels) {
+                                                          float *__restrict__ labels, Ragged rg) {
     __shared__ int wbest[4], wcnt[4];
     __shared__ float Ts[16];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);  // this pair's sizes; Nstr, Sstr: the strides
     int bc = -1, bi = 0x7fffffff;
     for (int s = tid; s < S; s += 256) {
-        const int c = counts[(size_t)b * S + s];
-        if (fitness) fitness[(size_t)b * S + s] = (float)c / (float)N;  // torch.mean of 0/1
+        const int c = counts[(size_t)b * Sstr + s];
+        if (fitness) fitness[(size_t)b * Sstr + s] = (float)c / (float)N;  // torch.mean of 0/1
         if (c > bc) { bc = c; bi = s; }  // strided ascending s: first max kept
     }
 #pragma unroll
@@ -872,26 +886,27 @@ __global__ __launch_bounds__(256) void select_best_kernel(const float *__restric
     __syncthreads();
     const int best = wbest[0];
     if (tid < 16) {
-        Ts[tid] = seed_trans[((size_t)b * S + best) * 16 + tid];
+        Ts[tid] = seed_trans[((size_t)b * Sstr + best) * 16 + tid];
         trans[(size_t)b * 16 + tid] = Ts[tid];
     }
     __syncthreads();
     float T[12];
 #pragma unroll
     for (int e = 0; e < 12; ++e) T[e] = Ts[e];
-    const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
+    const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
     for (int n = tid; n < N; n += 256) {
         const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
                                   tb[3 * n + 2]);
-        labels[(size_t)b * N + n] = (L2 < tau) ? 1.0f : 0.0f;
+        labels[(size_t)b * Nstr + n] = (L2 < tau) ? 1.0f : 0.0f;
     }
+    for (int n = N + tid; n < Nstr; n += 256) labels[(size_t)b * Nstr + n] = 0.0f;  // a ragged pair's padding
 }
 
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
                               const int *counts, int B, int N, int S, float tau, float *fitness,
-                              int *best, float *trans, float *labels, hipStream_t s) {
+                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg) {
     hipLaunchKernelGGL(select_best_kernel, dim3(B), dim3(256), 0, s, src, tgt, seed_trans, counts, N, S,
-                       tau, fitness, best, trans, labels);
+                       tau, fitness, best, trans, labels, rg);
     return hipGetLastError();
 }
 
@@ -956,12 +971,13 @@ PDSC_DEV void block_rigid(const float *__restrict__ A, const float *__restrict__
 // ---------------------------------------------------- a11 post-refinement
 __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ trans,
                                                          const float *__restrict__ src,
-                                                         const float *__restrict__ tgt, int N,
-                                                         float thr) {
+                                                         const float *__restrict__ tgt, int Nstr,
+                                                         float thr, Ragged rg) {
     __shared__ float red[RW][9];
     __shared__ float Ts[16];
     const int b = blockIdx.x, tid = threadIdx.x;
-    const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
+    const int N = rg.n(b, Nstr);  // this pair's correspondences; Nstr: the stride
+    const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
     if (tid < 16) Ts[tid] = trans[(size_t)b * 16 + tid];
     __syncthreads();
     int prev = 0;
@@ -996,8 +1012,8 @@ __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ tra
 }
 
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(post_refine_kernel, dim3(B), dim3(RB), 0, s, trans, src, tgt, N, thr);
+                              hipStream_t s, Ragged rg) {
+    hipLaunchKernelGGL(post_refine_kernel, dim3(B), dim3(RB), 0, s, trans, src, tgt, N, thr, rg);
     return hipGetLastError();
 }
 

@@ -120,12 +120,26 @@ inline PackLayout make_layout(int L, int in_dim) {
     return p;
 }
 
+// ---- ragged batches (pdsc_forward_testing_ragged) ----------------------------
+// Every pair's buffers keep the batch stride N (the largest pair); pair b uses
+// its first nv[b] rows and has sv[b] = int(nv[b] * ratio) seeds (S = the
+// largest).  nv == sv == nullptr: a uniform batch (every pair N rows, S seeds).
+struct Ragged {
+    const int *nv = nullptr, *sv = nullptr;
+    PDSC_DEV int n(int b, int N) const { return nv ? nv[b] : N; }
+    PDSC_DEV int s(int b, int S) const { return sv ? sv[b] : S; }
+};
+constexpr int RAGGED_CHUNK = 512;  // counts per setup launch (kernel-argument array)
+// counts (HOST, already validated) -> nv [B], sv [B] on the device, through
+// kernel arguments (no host-to-device copy of pageable memory on the stream)
+hipError_t launch_ragged_setup(const int32_t *counts_host, int B, double ratio, int *nv, int *sv, hipStream_t s);
+
 // ---- launchers --------------------------------------------------------------
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
-                         float *M, hipStream_t s);
+                         float *M, hipStream_t s, Ragged rg = {});
 // Mp: [B][mpack_floats(N)]
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
-                                float *Mp, hipStream_t s);
+                                float *Mp, hipStream_t s, Ragged rg = {});
 
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
                              const float *bn_rm, const float *bn_rv, int in, int out, bool f32, float *dst_w,
@@ -142,20 +156,20 @@ int attention_nsplit(int B, int N, bool f32);
 // vexp: [B][Npad/32] V-tile exponents of the H3 layout (attention_h3.hpp); unused for f32.
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
-                            hipStream_t s);
+                            hipStream_t s, Ragged rg = {});
 // attention_l fused with pw_mid_l (encoder.hip: attn_pw2_kernel) for this shape?
 bool attention_fused(int B, int N, bool f32);
 // attention of layer `layer` on (q, k, v, vexp_in) + the pointwise chain to the
 // layer-(layer+1) (qo, ko, vo, vexp_out), H3 layouts; feat updated in place.
 hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
                            const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
-                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s);
+                           float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s, Ragged rg = {});
 // attention of the last layer on (q, k, v, vexp_in) + its fc_message, residual,
 // F.normalize and classifier (encoder.hip: attn_pw2_last_kernel); outputs as launch_pw_last.
 hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, const void *q, const void *k,
                                 const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N,
                                 int Npad, const float *feat, float *feat_out, float *normed, _Float16 *normed_s,
-                                float *conf, hipStream_t s);
+                                float *conf, hipStream_t s, Ragged rg = {});
 // fp32 rows [B][N][CH] -> [B][Npad][CH], padding rows zero.
 hipError_t launch_pad_rows(const float *x, int B, int N, int Npad, float *y, hipStream_t s);
 // fp32 q, k, v [B][ld][CH] -> split layouts (rows N..Npad-1 zero).
@@ -167,7 +181,8 @@ hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, in
 
 // Pointwise chains (one workgroup per PT points); q, k, v in launch_attention's layouts.
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
-                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s);
+                           int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
+                           Ragged rg = {});
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
                          float *vexp, hipStream_t s);
@@ -176,36 +191,35 @@ hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, 
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s);
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
-                            float *lm, hipStream_t s);
+                            float *lm, hipStream_t s, Ragged rg = {});
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
-                            hipStream_t s);
+                            hipStream_t s, Ragged rg = {});
 
 // ns: normed as [B][N][2][128] fp16 hi/lo (qk_pos order, attention_h3.hpp)
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
-                           hipStream_t s);
+                           hipStream_t s, Ragged rg = {});
 hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStream_t s);
 // PDSC_PRECISION_F32 seed-row distances from the fp32 normed rows [B][N][128]
 hipError_t launch_knn_dist_f32(const float *normed, const int *seeds, int B, int N, int S, float *dist,
-                               hipStream_t s);
-// only: [B][S] flags, or null for every seed
+                               hipStream_t s, Ragged rg = {});
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s,
-                             const int *only = nullptr);
+                             Ragged rg = {});
 // feats: the split normed copy [B][N][2][128] fp16 (as launch_knn_dist reads it),
 // or the fp32 normed rows [B][N][128] when f32
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
                            int N, int S, int k, int T, const float *sigma, const float *sigma_d, float *hist,
-                           unsigned *seed_flags, hipStream_t s);
+                           unsigned *seed_flags, hipStream_t s, Ragged rg = {});
 hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T, bool batch_global,
-                             float *weights, int *iters_used, hipStream_t s);
+                             float *weights, int *iters_used, hipStream_t s, Ragged rg = {});
 // sums: scratch [B][S][15]
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             float *sums, hipStream_t s);
+                             float *sums, hipStream_t s, Ragged rg = {});
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
                               const int *counts, int B, int N, int S, float tau, float *fitness,
-                              int *best, float *trans, float *labels, hipStream_t s);
+                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg = {});
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
-                              hipStream_t s);
+                              hipStream_t s, Ragged rg = {});
 hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
                         hipStream_t s);
 

@@ -19,14 +19,16 @@ namespace pdsc {
 constexpr int SQ = 64;  // rows per workgroup
 
 __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict__ src,
-                                                        const float *__restrict__ conf, int N,
-                                                        float R2, float *__restrict__ lm) {
+                                                        const float *__restrict__ conf, int Nstr,
+                                                        float R2, float *__restrict__ lm, Ragged rg) {
     __shared__ f32x4 tile[256];
     __shared__ int part[4][SQ];
     const int b = blockIdx.y, tid = threadIdx.x, q = tid >> 6, il = tid & 63;
     const int i = blockIdx.x * SQ + il;
-    src += (size_t)b * N * 3;
-    conf += (size_t)b * N;
+    const int N = rg.n(b, Nstr);  // this pair's points; Nstr: the row stride
+    if (blockIdx.x * SQ >= N) return;  // workgroup-uniform
+    src += (size_t)b * Nstr * 3;
+    conf += (size_t)b * Nstr;
     float xi = 0, yi = 0, zi = 0, ci = 0;
     if (i < N) {
         xi = src[3 * i];
@@ -55,18 +57,21 @@ __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict_
     }
     part[q][il] = ok;
     __syncthreads();
-    if (q == 0 && i < N) lm[(size_t)b * N + i] = (part[0][il] & part[1][il] & part[2][il] & part[3][il]) ? 1.0f : 0.0f;
+    if (q == 0 && i < N) lm[(size_t)b * Nstr + i] = (part[0][il] & part[1][il] & part[2][il] & part[3][il]) ? 1.0f : 0.0f;
 }
 
 __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict__ conf,
-                                                        const float *__restrict__ lm, int N, int S,
-                                                        int *__restrict__ seeds) {
+                                                        const float *__restrict__ lm, int Nstr, int Sstr,
+                                                        int *__restrict__ seeds, Ragged rg) {
     __shared__ float ss[256];
     __shared__ int part[4][SQ];
     const int b = blockIdx.y, tid = threadIdx.x, q = tid >> 6, il = tid & 63;
     const int i = blockIdx.x * SQ + il;
-    conf += (size_t)b * N;
-    lm += (size_t)b * N;
+    // this pair's points and seeds; Nstr, Sstr: the strides of conf / lm and seeds
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    if (blockIdx.x * SQ >= N) return;  // workgroup-uniform
+    conf += (size_t)b * Nstr;
+    lm += (size_t)b * Nstr;
     const float si = (i < N) ? conf[i] * lm[i] : 0.0f;  // scores * is_local_max (:217)
     int rank = 0;
     for (int j0 = 0; j0 < N; j0 += 256) {
@@ -83,21 +88,21 @@ __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict_
     __syncthreads();
     if (q == 0 && i < N) {
         rank = part[0][il] + part[1][il] + part[2][il] + part[3][il];
-        if (rank < S) seeds[(size_t)b * S + rank] = i;
+        if (rank < S) seeds[(size_t)b * Sstr + rank] = i;
     }
 }
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
-                            float *lm, hipStream_t s) {
+                            float *lm, hipStream_t s, Ragged rg) {
     hipLaunchKernelGGL(local_max_kernel, dim3((N + SQ - 1) / SQ, B), dim3(256), 0, s, src, conf, N,
-                       sqrt_ge_threshold(radius), lm);
+                       sqrt_ge_threshold(radius), lm, rg);
     return hipGetLastError();
 }
 
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
-                            hipStream_t s) {
+                            hipStream_t s, Ragged rg) {
     hipLaunchKernelGGL(seed_rank_kernel, dim3((N + SQ - 1) / SQ, B), dim3(256), 0, s, conf, lm, N, S,
-                       seeds);
+                       seeds, rg);
     return hipGetLastError();
 }
 

@@ -282,6 +282,54 @@ def forward_stages(cfg, packed, corr_pos, src, tgt):
     return out
 
 
+def forward_ragged(cfg, packed, corr_pos, src, tgt, counts, debug=False):
+    """B pairs of different sizes in one call (pdsc_forward_testing_ragged): pair
+    b occupies the first counts[b] rows of the padded [B,N,.] inputs.  Returns
+    (final_trans [B,4,4], final_labels [B,N], rows past counts[b] zero); with
+    ``debug``, also the dict of stage outputs (conf, seeds, knn, weights,
+    trans_pre_refine) at the batch's strides."""
+    corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
+    B, N, _ = src.shape
+    _check_inputs(cfg, corr_pos, src, tgt)
+    counts = [int(c) for c in counts]
+    if len(counts) != B:
+        raise ValueError(f"{len(counts)} counts for {B} pairs")
+    dev = src.device
+    L = _lib.load()
+    nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
+    if nb == 0:
+        raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
+    ws = _workspace(nb, dev)
+    trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
+    labels = torch.empty((B, N), dtype=torch.float32, device=dev)
+    cnt = (ctypes.c_int32 * B)(*counts)
+    dbg, st = None, None
+    if debug:
+        S, k = int(N * cfg.ratio), min(cfg.k, N - 1)
+        f32, i32 = dict(dtype=torch.float32, device=dev), dict(dtype=torch.int32, device=dev)
+        st = {"conf": torch.empty((B, N), **f32), "seeds": torch.empty((B, S), **i32),
+              "knn": torch.empty((B, S, k), **i32), "weights": torch.empty((B, S, k), **f32),
+              "trans_pre_refine": torch.empty((B, 4, 4), **f32)}
+        dbg = _lib.PdscForwardDebug(*(st[n].data_ptr() for n in ("conf", "seeds", "knn", "weights",
+                                                                  "trans_pre_refine")))
+    check(L.pdsc_forward_testing_ragged(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N, cnt,
+                                        _p(trans), _p(labels), ctypes.byref(dbg) if dbg is not None else None, _p(ws),
+                                        nb, _stream(dev)), "pdsc_forward_testing_ragged")
+    return (trans, labels, st) if debug else (trans, labels)
+
+
+def pad_pairs(tensors, N=None):
+    """Stack [n_b, C] (or [1, n_b, C]) tensors into a zero-padded [B, N, C] batch
+    (N = the largest n_b by default); returns (batch, counts)."""
+    ts = [t[0] if t.dim() == 3 else t for t in tensors]
+    counts = [int(t.shape[0]) for t in ts]
+    N = max(counts) if N is None else int(N)
+    out = torch.zeros((len(ts), N, ts[0].shape[1]), dtype=ts[0].dtype, device=ts[0].device)
+    for b, t in enumerate(ts):
+        out[b, :t.shape[0]] = t
+    return out, counts
+
+
 def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=False):
     """Training-mode forward (models/PointDSC.py:158-163, :176, :182, :189-191) for
     B pairs: (final_trans [B,4,4], confidence [B,N], M [B,N,N] | None,

@@ -105,3 +105,20 @@ def test_query_functions_reject_bad_precision():
     assert lib.pdsc_attention_layout(4, 1000, 7, ctypes.byref(a), ctypes.byref(b)) == 1
     assert b"precision" in lib.pdsc_last_error()
     assert lib.pdsc_encoder_plan(4, 1000, -1, ctypes.byref(a)) == 1
+
+
+def test_ragged_counts_validated_on_host():
+    """pdsc_forward_testing_ragged rejects counts that would change a pair's k
+    (min(k, count - 1) must equal the batch's) or leave it without seeds, before
+    touching any buffer (dummy non-null pointers: nothing is dereferenced)."""
+    lib = _lib.load()
+    cfg = _lib.make_config()
+    dummy = ctypes.c_void_p(16)
+    for counts in ([1000, 40], [1000, 1001], [1000, 0]):
+        arr = (ctypes.c_int32 * 2)(*counts)
+        rc = lib.pdsc_forward_testing_ragged(ctypes.byref(cfg), dummy, dummy, dummy, dummy, 2, 1000, arr, dummy,
+                                             dummy, None, dummy, 1, None)
+        assert rc == 1 and b"counts[1]" in lib.pdsc_last_error(), counts
+    rc = lib.pdsc_forward_testing_ragged(ctypes.byref(cfg), dummy, dummy, dummy, dummy, 2, 1000, None, dummy,
+                                         dummy, None, dummy, 1, None)
+    assert rc == 1
