@@ -304,15 +304,29 @@ size_t pdsc_radius_knn_workspace_bytes(int32_t n);
 int32_t pdsc_radius_knn(const float *pts, int32_t n, float radius, int32_t max_nn, int32_t *nbr, double *dist2,
                         int32_t *count, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
 /* EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) (utils/pointcloud.py:
- * 20-21): smallest-eigenvalue eigenvector of the neighbourhood covariance,
- * (0,0,1) under 3 neighbours; oriented towards viewpoint (device float[3]) or,
- * when NULL, the cloud's centroid.                                          */
+ * 20-21) as open3d 0.9.0 (environment.yml:76) computes it with its default
+ * fast_normal_computation: the fp64 cumulant covariance of the neighbourhood,
+ * FastEigen3x3's smallest-eigenvalue eigenvector (A - l0 I)(A - l1 I) e0,
+ * normalised -- so its sign gives n_x >= 0 --, (0,0,1) when that vector is 0
+ * or under 3 neighbours.  orient (enum pdsc_normal_orientation):
+ *   PDSC_NORMALS_OPEN3D    that sign, as open3d leaves it on a cloud without
+ *                          normals (the demo's case; viewpoint unused, may be NULL)
+ *   PDSC_NORMALS_VIEWPOINT flipped towards viewpoint (device float[3])
+ *   PDSC_NORMALS_CENTROID  flipped towards the cloud's centroid (makes FPFH
+ *                          invariant to rigid motions; not open3d's result)   */
+enum pdsc_normal_orientation {
+    PDSC_NORMALS_OPEN3D = 0,
+    PDSC_NORMALS_VIEWPOINT = 1,
+    PDSC_NORMALS_CENTROID = 2,
+};
 size_t pdsc_estimate_normals_workspace_bytes(int32_t n, int32_t max_nn);
-int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, const float *viewpoint,
-                              float *normals, void *workspace, size_t workspace_bytes, pdsc_stream_t stream);
-/* VoxelDownSample(voxel_size): per-voxel means (normals averaged, then
- * normalised; normals / out_normals may be NULL), voxels in ascending key
- * order; out_pts [n,3] capacity; *out_count (device int32) = voxels.         */
+int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, int32_t orient,
+                              const float *viewpoint, float *normals, void *workspace, size_t workspace_bytes,
+                              pdsc_stream_t stream);
+/* VoxelDownSample(voxel_size): per-voxel means; normals summed and normalised
+ * (open3d's AccumulatedPoint::GetAverageNormal: a zero sum stays 0);
+ * normals / out_normals may be NULL; voxels in ascending key order; out_pts
+ * [n,3] capacity; *out_count (device int32) = voxels.                        */
 size_t pdsc_voxel_down_sample_workspace_bytes(int32_t n);
 int32_t pdsc_voxel_down_sample(const float *pts, const float *normals, int32_t n, float voxel_size, float *out_pts,
                                float *out_normals, int32_t *out_count, void *workspace, size_t workspace_bytes,

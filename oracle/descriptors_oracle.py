@@ -10,10 +10,13 @@ open3d's published algorithms (open3d 0.x, not installed here and not
 vendored in the reference: PARITY UNPINNED against open3d itself).  The
 restatement fixes the choices open3d leaves to its containers (hash-map
 voxel order -> ascending voxel key; nanoflann tie order -> ascending
-(d^2, index), the query first; unoriented normals -> towards a viewpoint,
-by default the cloud's centroid) exactly as include/pdsc.h documents them,
-and evaluates every sum in the same order as the kernels, so index outputs
-are compared bit-exactly and floating outputs to the last few ulps.
+(d^2, index), the query first) exactly as include/pdsc.h documents them, and
+evaluates every sum in the same order as the kernels, so index outputs are
+compared bit-exactly and floating outputs to the last few ulps.  Normals:
+open3d 0.9.0's (environment.yml:76) EstimateNormals with its default
+fast_normal_computation -- FastEigen3x3, whose eigenvector
+(A - l0 I)(A - l1 I) e0 carries the sign n_x >= 0 -- optionally flipped
+towards a viewpoint or the centroid.
 """
 import numpy as np
 
@@ -49,11 +52,49 @@ def voxel_down_sample(pts, voxel_size, normals=None):
     out = (_seq_group_sum(p, start, count) / count[:, None]).astype(np.float32)
     on = None
     if normals is not None:
-        a = _seq_group_sum(np.asarray(normals, np.float32).astype(np.float64)[order], start, count) / count[:, None]
-        nn = np.sqrt(a[:, 0] * a[:, 0] + a[:, 1] * a[:, 1] + a[:, 2] * a[:, 2])
-        inv = np.where(nn > 0, 1.0 / np.where(nn > 0, nn, 1.0), 1.0)
-        on = np.where(nn[:, None] > 0, a * inv[:, None], a).astype(np.float32)
+        # AccumulatedPoint::GetAverageNormal: the SUM, normalized() (v / sqrt(squaredNorm), 0 stays 0)
+        a = _seq_group_sum(np.asarray(normals, np.float32).astype(np.float64)[order], start, count)
+        on = _normalized(a).astype(np.float32)
     return out, on, uk
+
+
+def _normalized(v):
+    """Eigen's normalized() row-wise: v / sqrt((x x + y y) + z z); zero rows unchanged."""
+    z = (v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2]
+    n = np.sqrt(np.where(z > 0, z, 1.0))
+    return np.where(z[:, None] > 0, v / n[:, None], v)
+
+
+def fast_eigen3x3(C):
+    """open3d 0.9.0 FastEigen3x3 (geometry/EstimateNormals.cpp) on [n,3,3] fp64:
+    eigenvalues in closed form (l0 >= l1 >= l2), the eigenvector of l2 as
+    (A - l0 I)(A - l1 I) e0 normalised, 0 where it vanishes -- each operation in
+    the order of the kernel (pointdsc_amd/csrc/descriptors.hip)."""
+    a00, a11, a22 = C[:, 0, 0], C[:, 1, 1], C[:, 2, 2]
+    a01, a02, a12 = C[:, 0, 1], C[:, 0, 2], C[:, 1, 2]
+    p1 = a01 * a01 + a02 * a02 + a12 * a12
+    diag = p1 == 0.0
+    with np.errstate(all="ignore"):
+        q = ((a00 + a11) + a22) / 3.0
+        d0, d1, d2 = a00 - q, a11 - q, a22 - q
+        p = np.sqrt((((d0 * d0 + d1 * d1) + d2 * d2) + 2 * p1) / 6.0)
+        ip = 1.0 / p
+        b00, b11, b22, b01, b02, b12 = ip * d0, ip * d1, ip * d2, ip * a01, ip * a02, ip * a12
+        det = (b00 * (b11 * b22 - b12 * b12) - b01 * (b01 * b22 - b02 * b12)) + b02 * (b01 * b12 - b02 * b11)
+        r = det / 2.0
+        phi = np.where(r <= -1, np.pi / 3.0, np.where(r >= 1, 0.0, np.arccos(np.clip(r, -1, 1)) / 3.0))
+        l0 = q + 2.0 * p * np.cos(phi)
+        l2 = q + 2.0 * p * np.cos(phi + 2.0 * np.pi / 3.0)
+        l1 = q * 3.0 - l0 - l2
+    dl2 = np.minimum(a00, np.minimum(a11, a22))
+    dl0 = np.maximum(a00, np.maximum(a11, a22))
+    dl1 = ((a00 + a11) + a22) - dl0 - dl2
+    l0, l1 = np.where(diag, dl0, l0), np.where(diag, dl1, l1)
+    c0, c1, c2 = a00 - l1, a01, a02
+    m00, m11, m22 = a00 - l0, a11 - l0, a22 - l0
+    v = np.stack([(m00 * c0 + a01 * c1) + a02 * c2, (a01 * c0 + m11 * c1) + a12 * c2,
+                  (a02 * c0 + a12 * c1) + m22 * c2], 1)
+    return _normalized(v)
 
 
 def _d2(q, p):
@@ -101,12 +142,16 @@ def radius_knn(pts, radius, max_nn, chunk=256, queries=None):
     return nbr, d2o, cnt
 
 
-def estimate_normals(pts, radius, max_nn=30, viewpoint=None, queries=None):
-    """EstimateNormals: smallest-eigenvalue eigenvector of the fp64 cumulant
-    covariance, (0,0,1) under 3 neighbours, sign towards the viewpoint (default
-    centroid).  Returns (normals fp32 [q,3], eigenvalues [q,3] ascending) for
-    the points `queries` (default: all)."""
+def estimate_normals(pts, radius, max_nn=30, viewpoint=None, queries=None, orient=None):
+    """EstimateNormals as open3d 0.9 computes it (fast_eigen3x3 of the fp64
+    cumulant covariance; (0,0,1) under 3 neighbours or for a zero vector), with
+    open3d's sign (orient 'open3d', the default without a viewpoint), or flipped
+    towards `viewpoint` ('viewpoint') or the cloud's centroid ('centroid').
+    Returns (normals fp32 [q,3], eigenvalues [q,3] ascending) for the points
+    `queries` (default: all)."""
     cloud = np.asarray(pts, np.float32)
+    if orient is None:
+        orient = "viewpoint" if viewpoint is not None else "open3d"
     qidx = np.arange(len(cloud)) if queries is None else np.asarray(queries, np.int64)
     nbr, _, cnt = radius_knn(cloud, radius, max_nn, queries=qidx)
     p = cloud[qidx]
@@ -126,13 +171,14 @@ def estimate_normals(pts, radius, max_nn=30, viewpoint=None, queries=None):
     C[:, 0, 1] = C[:, 1, 0] = s[:, 4] - s[:, 0] * s[:, 1]
     C[:, 0, 2] = C[:, 2, 0] = s[:, 5] - s[:, 0] * s[:, 2]
     C[:, 1, 2] = C[:, 2, 1] = s[:, 7] - s[:, 1] * s[:, 2]
-    w, V = np.linalg.eigh(C)
-    nv = V[:, :, 0]
-    zero = (cnt < 3) | np.all(C.reshape(n, 9) == 0, 1)
+    w = np.linalg.eigvalsh(C)
+    nv = fast_eigen3x3(C)
+    zero = (cnt < 3) | np.all(nv == 0, 1)
     nv[zero] = (0.0, 0.0, 1.0)
-    vp = cloud.astype(np.float64).mean(0) if viewpoint is None else np.asarray(viewpoint, np.float64)
-    flip = np.sum(nv * (vp - p.astype(np.float64)), 1) < 0
-    nv[flip] *= -1
+    if orient != "open3d":
+        vp = cloud.astype(np.float64).mean(0) if orient == "centroid" else np.asarray(viewpoint, np.float64)
+        flip = np.sum(nv * (vp - p.astype(np.float64)), 1) < 0
+        nv[flip] *= -1
     return nv.astype(np.float32), w
 
 

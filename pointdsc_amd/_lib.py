@@ -106,7 +106,7 @@ _PROTOS = {
     "pdsc_radius_knn_workspace_bytes": (c_size_t, [c_int32]),
     "pdsc_radius_knn": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_estimate_normals_workspace_bytes": (c_size_t, [c_int32, c_int32]),
-    "pdsc_estimate_normals": (c_int32, [vp, c_int32, c_float, c_int32, vp, vp, vp, c_size_t, vp]),
+    "pdsc_estimate_normals": (c_int32, [vp, c_int32, c_float, c_int32, c_int32, vp, vp, vp, c_size_t, vp]),
     "pdsc_voxel_down_sample_workspace_bytes": (c_size_t, [c_int32]),
     "pdsc_voxel_down_sample": (c_int32, [vp, vp, c_int32, c_float, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_compute_fpfh_workspace_bytes": (c_size_t, [c_int32, c_int32]),

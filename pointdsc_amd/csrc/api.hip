@@ -803,10 +803,13 @@ size_t pdsc_estimate_normals_workspace_bytes(int32_t n, int32_t max_nn) {
     return grid_workspace_bytes(n) + align_bytes((size_t)n * max_nn * sizeof(int)) + align_bytes((size_t)n * sizeof(int));
 }
 
-int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, const float *viewpoint,
-                              float *normals, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
+int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t max_nn, int32_t orient,
+                              const float *viewpoint, float *normals, void *ws, size_t ws_bytes, pdsc_stream_t stream) {
     RET_IF(check_cloud(pts, n, radius, max_nn));
     if (!normals || !ws) return fail(PDSC_ERR_ARG, "null pointer");
+    if (orient != PDSC_NORMALS_OPEN3D && orient != PDSC_NORMALS_VIEWPOINT && orient != PDSC_NORMALS_CENTROID)
+        return fail(PDSC_ERR_ARG, "orient=%d (enum pdsc_normal_orientation)", orient);
+    if (orient == PDSC_NORMALS_VIEWPOINT && !viewpoint) return fail(PDSC_ERR_ARG, "PDSC_NORMALS_VIEWPOINT needs a viewpoint");
     RET_IF(need_ws(ws_bytes, pdsc_estimate_normals_workspace_bytes(n, max_nn)));
     hipStream_t s = S_(stream);
     char *w = static_cast<char *>(ws);
@@ -815,7 +818,7 @@ int32_t pdsc_estimate_normals(const float *pts, int32_t n, float radius, int32_t
     GridBufs G;
     HIPCHK(build_grid(pts, n, radius, 0.0, ws, G, s));
     HIPCHK(launch_radius_knn(pts, n, G, radius, max_nn, nbr, nullptr, cnt, s));
-    HIPCHK(launch_normals(pts, n, nbr, cnt, max_nn, G, viewpoint, normals, s));
+    HIPCHK(launch_normals(pts, n, nbr, cnt, max_nn, G, orient, viewpoint, normals, s));
     return grid_status(G, s);
 }
 

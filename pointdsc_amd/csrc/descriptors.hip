@@ -287,29 +287,66 @@ __global__ __launch_bounds__(KNN_WPB * 64) void radius_knn_kernel(const float *_
 }
 
 // ----------------------------------------------------------------- normals
-// Smallest-eigenvalue eigenvector of a symmetric 3x3 (cyclic Jacobi, fp64).
-PDSC_DEV D3 sym3_min_eigvec(double a00, double a11, double a22, double a01, double a02, double a12) {
-    D3 v0 = d3(1, 0, 0), v1 = d3(0, 1, 0), v2 = d3(0, 0, 1);
-    for (int sweep = 0; sweep < 12; ++sweep) {
-        const double off = a01 * a01 + a02 * a02 + a12 * a12;
-        const double dia = a00 * a00 + a11 * a11 + a22 * a22;
-        if (off <= 1e-30 * dia || off == 0.0) break;
-        jrot(a00, a11, a01, a02, a12, v0, v1);
-        jrot(a00, a22, a02, a01, a12, v0, v2);
-        jrot(a11, a22, a12, a01, a02, v1, v2);
+// open3d 0.9.0's FastEigen3x3 (EstimateNormals.cpp; `fast_normal_computation`,
+// true by default in estimate_normals): the eigenvalues of the symmetric 3x3 A
+// in closed form (largest l0, middle l1, smallest l2; Wikipedia "Eigenvalue
+// algorithm", 3x3 symmetric) and the smallest one's eigenvector as
+// (A - l0 I)(A - l1 I) e0 -- Cayley-Hamilton: that column lies in the l2
+// eigenspace -- normalised, or 0 when it vanishes.  In exact arithmetic it is
+// (l2 - l0)(l2 - l1)(v2 . e0) v2, so the sign open3d returns makes n_x >= 0.
+// Every operation in open3d's order (Eigen's 3x3 determinant and product as
+// sums left to right; the library builds without fma contraction, as does this
+// file: -ffp-contract=off).
+// Eigen's normalized(): v / sqrt(squaredNorm), unchanged when that is 0.
+PDSC_DEV double o3d_normalize(D3 &v) {
+    const double z = (v.x * v.x + v.y * v.y) + v.z * v.z;
+    if (z > 0) {
+        const double n = sqrt(z);
+        v = d3(v.x / n, v.y / n, v.z / n);
     }
-    D3 v = v0;
-    double l = a00;
-    if (a11 < l) {
-        l = a11;
-        v = v1;
+    return z;
+}
+PDSC_DEV D3 o3d09_fast_eigen3x3(double a00, double a11, double a22, double a01, double a02, double a12) {
+    const double p1 = a01 * a01 + a02 * a02 + a12 * a12;
+    double l0, l1, l2;
+    if (p1 == 0.0) {
+        l2 = fmin(a00, fmin(a11, a22));
+        l0 = fmax(a00, fmax(a11, a22));
+        l1 = ((a00 + a11) + a22) - l0 - l2;  // A.trace() - l0 - l2
+    } else {
+        const double q = ((a00 + a11) + a22) / 3.0;
+        const double d0 = a00 - q, d1 = a11 - q, d2 = a22 - q;
+        const double p2 = ((d0 * d0 + d1 * d1) + d2 * d2) + 2 * p1;
+        const double p = sqrt(p2 / 6.0);
+        const double ip = 1.0 / p;  // B = (1 / p) (A - q I)
+        const double b00 = ip * d0, b11 = ip * d1, b22 = ip * d2, b01 = ip * a01, b02 = ip * a02, b12 = ip * a12;
+        // Eigen's 3x3 determinant: m00 (m11 m22 - m12 m21) - m10 (m01 m22 - m02 m21) + m20 (m01 m12 - m02 m11)
+        const double det = (b00 * (b11 * b22 - b12 * b12) - b01 * (b01 * b22 - b02 * b12)) + b02 * (b01 * b12 - b02 * b11);
+        const double r = det / 2.0;
+        double phi;
+        if (r <= -1)
+            phi = M_PI / 3.0;
+        else if (r >= 1)
+            phi = 0.0;
+        else
+            phi = acos(r) / 3.0;
+        l0 = q + 2.0 * p * cos(phi);
+        l2 = q + 2.0 * p * cos(phi + 2.0 * M_PI / 3.0);
+        l1 = q * 3.0 - l0 - l2;
     }
-    if (a22 < l) v = v2;
+    // (A - l0 I) (A.col(0) - (l1, 0, 0))
+    const double c0 = a00 - l1, c1 = a01, c2 = a02;
+    const double m00 = a00 - l0, m11 = a11 - l0, m22 = a22 - l0;
+    D3 v = d3((m00 * c0 + a01 * c1) + a02 * c2, (a01 * c0 + m11 * c1) + a12 * c2, (a02 * c0 + a12 * c1) + m22 * c2);
+    if (o3d_normalize(v) == 0.0) return d3(0, 0, 0);
     return v;
 }
 
+// orient: PDSC_NORMALS_OPEN3D (the eigenvector's own sign, as open3d 0.9 leaves
+// it on a cloud without normals), _VIEWPOINT (towards viewpoint), _CENTROID
+// (towards the cloud's centroid)
 __global__ void normals_kernel(const float *__restrict__ pts, int n, const int *__restrict__ nbr,
-                               const int *__restrict__ cnt, int K, const CloudStats *st,
+                               const int *__restrict__ cnt, int K, const CloudStats *st, int orient,
                                const float *__restrict__ viewpoint, float *__restrict__ nrm) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -335,16 +372,17 @@ __global__ void normals_kernel(const float *__restrict__ pts, int n, const int *
         s0 /= inv, s1 /= inv, s2 /= inv, s3 /= inv, s4 /= inv, s5 /= inv, s6 /= inv, s7 /= inv, s8 /= inv;
         const double a00 = s3 - s0 * s0, a11 = s6 - s1 * s1, a22 = s8 - s2 * s2;
         const double a01 = s4 - s0 * s1, a02 = s5 - s0 * s2, a12 = s7 - s1 * s2;
-        if (a00 != 0 || a11 != 0 || a22 != 0 || a01 != 0 || a02 != 0 || a12 != 0) {
-            D3 v = sym3_min_eigvec(a00, a11, a22, a01, a02, a12);
-            if (normalize3(v) > 0) nv = v;
-        }
+        const D3 v = o3d09_fast_eigen3x3(a00, a11, a22, a01, a02, a12);
+        if (v.x != 0.0 || v.y != 0.0 || v.z != 0.0) nv = v;  // a zero vector -> (0, 0, 1) (EstimateNormals)
     }
-    const float *p = pts + 3 * (size_t)i;
-    const double vx = viewpoint ? (double)viewpoint[0] : st->centroid[0];
-    const double vy = viewpoint ? (double)viewpoint[1] : st->centroid[1];
-    const double vz = viewpoint ? (double)viewpoint[2] : st->centroid[2];
-    if (nv.x * (vx - p[0]) + nv.y * (vy - p[1]) + nv.z * (vz - p[2]) < 0) nv = d3(-nv.x, -nv.y, -nv.z);
+    if (orient != PDSC_NORMALS_OPEN3D) {
+        const float *p = pts + 3 * (size_t)i;
+        const bool vpt = orient == PDSC_NORMALS_VIEWPOINT;
+        const double vx = vpt ? (double)viewpoint[0] : st->centroid[0];
+        const double vy = vpt ? (double)viewpoint[1] : st->centroid[1];
+        const double vz = vpt ? (double)viewpoint[2] : st->centroid[2];
+        if (nv.x * (vx - p[0]) + nv.y * (vy - p[1]) + nv.z * (vz - p[2]) < 0) nv = d3(-nv.x, -nv.y, -nv.z);
+    }
     nrm[3 * (size_t)i + 0] = (float)nv.x;
     nrm[3 * (size_t)i + 1] = (float)nv.y;
     nrm[3 * (size_t)i + 2] = (float)nv.z;
@@ -377,8 +415,8 @@ __global__ void voxel_reduce_kernel(const float *__restrict__ pts, const float *
     opts[3 * (size_t)v + 1] = (float)(py / dm);
     opts[3 * (size_t)v + 2] = (float)(pz / dm);
     if (nrm && onrm) {
-        D3 a = d3(nx / dm, ny / dm, nz / dm);
-        normalize3(a);
+        D3 a = d3(nx, ny, nz);  // open3d: normal_.normalized() of the sum (a zero sum stays 0)
+        o3d_normalize(a);
         onrm[3 * (size_t)v] = (float)a.x;
         onrm[3 * (size_t)v + 1] = (float)a.y;
         onrm[3 * (size_t)v + 2] = (float)a.z;
@@ -573,9 +611,9 @@ hipError_t launch_radius_knn(const float *pts, int n, const GridBufs &G, double 
 }
 
 hipError_t launch_normals(const float *pts, int n, const int *nbr, const int *cnt, int K, const GridBufs &G,
-                          const float *viewpoint, float *nrm, hipStream_t s) {
-    hipLaunchKernelGGL(normals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, nbr, cnt, K, G.st, viewpoint,
-                       nrm);
+                          int orient, const float *viewpoint, float *nrm, hipStream_t s) {
+    hipLaunchKernelGGL(normals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pts, n, nbr, cnt, K, G.st, orient,
+                       viewpoint, nrm);
     return hipGetLastError();
 }
 

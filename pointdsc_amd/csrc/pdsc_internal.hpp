@@ -249,7 +249,7 @@ hipError_t build_grid(const float *pts, int n, double cell, double half, void *w
 hipError_t launch_radius_knn(const float *pts, int n, const GridBufs &G, double radius, int K, int *nbr, double *d2,
                              int *cnt, hipStream_t s);
 hipError_t launch_normals(const float *pts, int n, const int *nbr, const int *cnt, int K, const GridBufs &G,
-                          const float *viewpoint, float *nrm, hipStream_t s);
+                          int orient, const float *viewpoint, float *nrm, hipStream_t s);
 hipError_t launch_voxel_reduce(const float *pts, const float *nrm, int n, const GridBufs &G, float *opts, float *onrm,
                                int *count, hipStream_t s);
 hipError_t launch_fpfh(const float *pts, const float *nrm, int n, const int *nbr, const int *cnt, const double *d2,

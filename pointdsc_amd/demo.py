@@ -48,18 +48,19 @@ def build_model(config: dict, weights: str | None, device):
     return model.to(device).eval()
 
 
-def register(model, pcd1, pcd2, downsample: float, device):
+def register(model, pcd1, pcd2, downsample: float, device, orient: str = "open3d"):
     """The demo's pipeline for two clouds (paths or [n,3] arrays): returns a dict
     with final_trans [4,4], final_labels [n], the correspondence inputs and the
-    downsampled points / features of both clouds."""
+    downsampled points / features of both clouds.  orient: the normals' sign
+    (descriptors.estimate_normals; 'open3d' = the reference's)."""
     from . import descriptors as D
     from .correspondence import build_correspondences
 
     def feats(pcd):
         if isinstance(pcd, str):
-            return D.extract_fpfh_features(pcd, downsample, device)
+            return D.extract_fpfh_features(pcd, downsample, device, orient)
         raw = torch.as_tensor(np.asarray(pcd, np.float32)).to(device)
-        nrm = D.estimate_normals(raw, radius=downsample * 2, max_nn=30)
+        nrm = D.estimate_normals(raw, radius=downsample * 2, max_nn=30, orient=orient)
         pts, pn = D.voxel_down_sample(raw, downsample, nrm)
         return raw, pts, D.compute_fpfh(pts, pn, radius=downsample * 5, max_nn=100)[1]
 
@@ -83,6 +84,8 @@ def main(argv=None):
     ap.add_argument("--config", default=None, help="a snapshot config.json (default: the 3DMatch release values)")
     ap.add_argument("--weights", default=None, help="state dict (torch.load weights_only=True)")
     ap.add_argument("--out", default=None, help="write the result arrays to this .npz")
+    ap.add_argument("--normals", default="open3d", choices=["open3d", "centroid"],
+                    help="normal sign: open3d 0.9's (the reference's) or towards the cloud's centroid")
     a = ap.parse_args(argv)
     if a.descriptor != "fpfh":
         sys.exit("descriptor 'fcgf' needs MinkowskiEngine and the FCGF checkpoint: out of scope (use --descriptor fpfh)")
@@ -94,7 +97,7 @@ def main(argv=None):
             config.update({k: v for k, v in json.load(f).items() if k in RELEASE_3DMATCH})
     device = torch.device("cuda")
     model = build_model(config, a.weights, device)
-    res = register(model, a.pcd1, a.pcd2, config["downsample"], device)
+    res = register(model, a.pcd1, a.pcd2, config["downsample"], device, a.normals)
     T = res["final_trans"].cpu().numpy()
     print(f"{len(res['corr'])} correspondences, {int((res['final_labels'] > 0).sum())} inliers")
     print("final_trans =\n" + np.array2string(T, precision=6, suppress_small=True))

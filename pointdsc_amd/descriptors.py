@@ -50,10 +50,22 @@ def radius_knn(points: torch.Tensor, radius: float, max_nn: int):
     return nbr, d2, cnt
 
 
-def estimate_normals(points: torch.Tensor, radius: float, max_nn: int = 30, viewpoint=None) -> torch.Tensor:
+ORIENT = {"open3d": 0, "viewpoint": 1, "centroid": 2}  # enum pdsc_normal_orientation
+
+
+def estimate_normals(points: torch.Tensor, radius: float, max_nn: int = 30, viewpoint=None,
+                     orient: str | None = None) -> torch.Tensor:
     """pcd.estimate_normals(KDTreeSearchParamHybrid(radius, max_nn)) (utils/pointcloud.py:20-21):
-    unit normals [n,3], oriented towards `viewpoint` (3 floats) or the centroid."""
+    unit normals [n,3] with open3d 0.9's sign (its FastEigen3x3: n_x >= 0) by
+    default; orient='viewpoint' (or a `viewpoint` given) flips them towards
+    `viewpoint` (3 floats), orient='centroid' towards the cloud's centroid."""
     points = _dev(points, "points")
+    if orient is None:
+        orient = "viewpoint" if viewpoint is not None else "open3d"
+    if orient not in ORIENT:
+        raise ValueError(f"orient must be one of {sorted(ORIENT)}, got {orient!r}")
+    if orient == "viewpoint" and viewpoint is None:
+        raise ValueError("orient='viewpoint' needs a viewpoint")
     n = points.shape[0]
     L = _lib.load()
     nb = L.pdsc_estimate_normals_workspace_bytes(n, int(max_nn))
@@ -62,8 +74,8 @@ def estimate_normals(points: torch.Tensor, radius: float, max_nn: int = 30, view
     if viewpoint is not None:
         vp = torch.as_tensor(np.asarray(viewpoint, np.float32).reshape(3), device=points.device)
     out = torch.empty_like(points)
-    check(L.pdsc_estimate_normals(_p(points), n, float(radius), int(max_nn), _p(vp), _p(out), _p(ws), nb,
-                                  _stream(points.device)), "pdsc_estimate_normals")
+    check(L.pdsc_estimate_normals(_p(points), n, float(radius), int(max_nn), ORIENT[orient], _p(vp), _p(out), _p(ws),
+                                  nb, _stream(points.device)), "pdsc_estimate_normals")
     return out
 
 
@@ -106,13 +118,14 @@ def compute_fpfh(points: torch.Tensor, normals: torch.Tensor, radius: float, max
     return f, fn
 
 
-def extract_fpfh_features(pcd_path: str, downsample: float, device):
+def extract_fpfh_features(pcd_path: str, downsample: float, device, orient: str = "open3d"):
     """demo_registration.py:37-44 on the GPU: normals on the raw cloud (radius
-    2 v, 30 nearest), voxel downsample (normals averaged), FPFH (radius 5 v,
+    2 v, 30 nearest; open3d 0.9's unoriented sign), voxel downsample (normals
+    summed and normalised), FPFH (radius 5 v,
     100 nearest), L2-normalised.  Returns (raw points [n,3], downsampled
     points [m,3], features fp32 [m,33]) as device tensors."""
     raw = torch.from_numpy(read_ply(pcd_path)).to(device)
-    nrm = estimate_normals(raw, radius=downsample * 2, max_nn=30)
+    nrm = estimate_normals(raw, radius=downsample * 2, max_nn=30, orient=orient)
     pts, pn = voxel_down_sample(raw, downsample, nrm)
     _, feats = compute_fpfh(pts, pn, radius=downsample * 5, max_nn=100)
     return raw, pts, feats

@@ -31,10 +31,12 @@ COLUMNS = ["success", "re_deg", "te_cm", "input_inliers", "input_inlier_ratio", 
 THRESHOLDS = {"3dmatch": (15.0, 30.0), "kitti": (5.0, 60.0)}  # (re_thre deg, te_thre cm)
 
 
-def pair_stats(trans, gt_trans, pred_labels, gt_labels, re_thre=15.0, te_thre=30.0):
+def pair_stats(trans, gt_trans, pred_labels, gt_labels, re_thre=15.0, te_thre=30.0, counts=None):
     """[B, 9] float64 rows (columns 0-8) for a batch of B pairs.
 
-    trans, gt_trans [B,4,4]; pred_labels, gt_labels [B,N] (0/1)."""
+    trans, gt_trans [B,4,4]; pred_labels, gt_labels [B,N] (0/1); counts: each
+    pair's correspondences when the batch is ragged (labels zero-padded past
+    them), else every pair has N."""
     trans, gt_trans = trans.float(), gt_trans.float()
     R, t = trans[:, :3, :3], trans[:, :3, 3]
     gR, gt_t = gt_trans[:, :3, :3], gt_trans[:, :3, 3]
@@ -52,7 +54,11 @@ def pair_stats(trans, gt_trans, pred_labels, gt_labels, re_thre=15.0, te_thre=30
     recall = torch.where(n_in > 0, tp / n_in.clamp(min=1), torch.zeros_like(tp))
     denom = precision + recall
     f1 = torch.where(denom > 0, 2 * precision * recall / denom.clamp(min=1e-300), torch.zeros_like(tp))
-    ratio = gt_labels.float().mean(-1).double()
+    if counts is None:
+        ratio = gt_labels.float().mean(-1).double()  # torch.mean of the 0/1 labels
+    else:
+        # the same fp32 sum / count the unpadded mean computes
+        ratio = (n_in.float() / torch.as_tensor(counts, dtype=torch.float32, device=n_in.device)).double()
     return torch.stack([success, re.double(), te.double(), n_in, ratio, tp, precision, recall, f1], dim=1)
 
 
@@ -130,33 +136,58 @@ def save_outputs(stats, log_path=None, npy_path=None, n_scenes=None):
         np.save(npy_path, np.asarray(stats, dtype=np.float64), allow_pickle=False)
 
 
+def pair_sizes(n_pairs, num_corr, seed=0):
+    """Per-pair correspondence counts: num_corr for every pair, or, for a (lo, hi)
+    range, pair i's count drawn from U{lo..hi} by its own seed (so every rank
+    and every batching of the job sees the same sizes) -- the varying N of the
+    reference's evaluation sets (datasets/ThreeDMatch.py:268-290)."""
+    if isinstance(num_corr, int):
+        return [num_corr] * n_pairs
+    lo, hi = (int(x) for x in num_corr)
+    return [int(np.random.RandomState(seed * 100003 + i + 7).randint(lo, hi + 1)) for i in range(n_pairs)]
+
+
 def evaluate_synthetic(model, n_pairs, num_corr, preset="3dmatch", batch=16, seed=0, device=None,
                        inlier_ratio=0.3):
     """Sharded evaluation over n_pairs synthetic pairs: rank r evaluates pairs
-    r, r+W, ... in batches through the batched forward, then the [n_pairs, 12]
-    stats matrix is all-gathered.  Returns (stats numpy, summary dict)."""
+    r, r+W, ... in batches through the batched forward (the ragged forward,
+    PointDSC.forward_list, when num_corr is a (lo, hi) range of sizes), then the
+    [n_pairs, 12] stats matrix is all-gathered.  Returns (stats numpy, summary dict)."""
     import time
-    from . import dist
+    from . import dist, kernels
     from .synthetic import synthetic_pair
     rank, W = dist.world()
     mine = dist.shard_indices(n_pairs, rank, W)
+    sizes = pair_sizes(n_pairs, num_corr, seed)
     re_thre, te_thre = THRESHOLDS[preset]
     rows = []
     for b0 in range(0, len(mine), batch):
         idx = mine[b0:b0 + batch]
         t0 = time.perf_counter()
-        ps = [synthetic_pair(num_corr, seed * 100003 + i, preset=preset, inlier_ratio=inlier_ratio) for i in idx]
-        corr, src, tgt, gtT, gtL = (torch.from_numpy(np.stack([p[k] for p in ps])).to(device)
-                                    for k in ("corr_pos", "src_keypts", "tgt_keypts", "gt_trans", "gt_labels"))
+        ps = [synthetic_pair(sizes[i], seed * 100003 + i, preset=preset, inlier_ratio=inlier_ratio) for i in idx]
+        counts = [sizes[i] for i in idx]
+        ragged = len(set(counts)) > 1
+        if ragged:
+            corr, src, tgt, gtL = (kernels.pad_pairs([torch.from_numpy(p[k][:, None] if p[k].ndim == 1 else p[k])
+                                                      for p in ps])[0].to(device)
+                                   for k in ("corr_pos", "src_keypts", "tgt_keypts", "gt_labels"))
+            gtL = gtL[..., 0]
+            gtT = torch.from_numpy(np.stack([p["gt_trans"] for p in ps])).to(device)
+        else:
+            corr, src, tgt, gtT, gtL = (torch.from_numpy(np.stack([p[k] for p in ps])).to(device)
+                                        for k in ("corr_pos", "src_keypts", "tgt_keypts", "gt_trans", "gt_labels"))
         if device is not None and device.type == "cuda":
             torch.cuda.synchronize(device)
         t_data = (time.perf_counter() - t0) / len(idx)
         t0 = time.perf_counter()
-        T, L = model.forward_batched(corr, src, tgt)
+        if ragged:
+            T, L = kernels.forward_ragged(model.pdsc_config(), model.packed_weights(), corr, src, tgt, counts)
+        else:
+            T, L = model.forward_batched(corr, src, tgt)
         if device is not None and device.type == "cuda":
             torch.cuda.synchronize(device)
         t_model = (time.perf_counter() - t0) / len(idx)
-        st = pair_stats(T, gtT, L, gtL, re_thre, te_thre).cpu()
+        st = pair_stats(T, gtT, L, gtL, re_thre, te_thre, counts if ragged else None).cpu()
         extra = torch.tensor([[t_model, t_data, 0.0]], dtype=torch.float64).expand(len(idx), 3)
         rows.append(torch.cat([st, extra], dim=1))
     mine_rows = torch.cat(rows) if rows else torch.zeros((0, 12), dtype=torch.float64)
@@ -177,7 +208,7 @@ def main():
     from .synthetic import PRESETS, trained_state_dict
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=64)
-    ap.add_argument("--num-corr", type=int, default=1000)
+    ap.add_argument("--num-corr", default="1000", help="N, or LO:HI for per-pair sizes in that range (ragged batches)")
     ap.add_argument("--preset", default="3dmatch", choices=list(PRESETS))
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--inlier-ratio", type=float, default=0.3)
@@ -196,7 +227,8 @@ def main():
                  nms_radius=p["nms_radius"])
     m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict(a.preset).items()})
     m = m.to(dev).eval()
-    stats, summary = evaluate_synthetic(m, a.pairs, a.num_corr, a.preset, a.batch, device=dev,
+    nc = tuple(int(x) for x in a.num_corr.split(":")) if ":" in a.num_corr else int(a.num_corr)
+    stats, summary = evaluate_synthetic(m, a.pairs, nc, a.preset, a.batch, device=dev,
                                         inlier_ratio=a.inlier_ratio)
     if not tdist.is_initialized() or tdist.get_rank() == 0:
         save_outputs(stats, a.log, a.save_npy)

@@ -93,8 +93,8 @@ def test_oracle_pair_features_and_fpfh_rigid_invariance():
     p = np.stack([u, v, 0.2 * np.sin(3 * u) * np.cos(2 * v)], 1).astype(np.float32)
     R, t = _rigid(1)
     q = (p.astype(np.float64) @ R.T + t).astype(np.float32)
-    n1, _ = DO.estimate_normals(p, 0.1, 30)
-    n2, _ = DO.estimate_normals(q, 0.1, 30)
+    n1, _ = DO.estimate_normals(p, 0.1, 30, orient="centroid")
+    n2, _ = DO.estimate_normals(q, 0.1, 30, orient="centroid")
     np.testing.assert_allclose(n1.astype(np.float64) @ R.T, n2, atol=1e-4)
     f1, _ = DO.compute_fpfh(p, n1, 0.25, 100)
     f2, _ = DO.compute_fpfh(q, n2, 0.25, 100)
@@ -103,3 +103,29 @@ def test_oracle_pair_features_and_fpfh_rigid_invariance():
     a0, a1, a2 = DO.pair_features(np.zeros((1, 3)), np.array([[0, 0, 1.0]]), np.array([[1.0, 0, 0]]),
                                   np.array([[0, 0, 1.0]]))
     assert abs(a0[0]) < 1e-15 and abs(a1[0]) < 1e-15 and abs(a2[0]) < 1e-15
+
+
+def test_oracle_open3d_fast_eigen_sign():
+    """open3d 0.9's FastEigen3x3 (the normals of its default estimate_normals):
+    the smallest-eigenvalue eigenvector up to fp64 rounding, its sign n_x >= 0
+    (it is (l2 - l0)(l2 - l1)(v2 . e0) v2 before normalisation); a diagonal
+    covariance whose smallest entry is not a00 gives the zero vector, which
+    EstimateNormals replaces by (0, 0, 1)."""
+    rng = np.random.RandomState(9)
+    A = rng.randn(500, 3, 3)
+    C = A @ A.transpose(0, 2, 1)
+    v = DO.fast_eigen3x3(C)
+    w, V = np.linalg.eigh(C)
+    assert np.all(np.abs(np.sum(v * V[:, :, 0], 1)) > 1 - 1e-9)
+    assert np.all(v[:, 0] >= 0)
+    D = np.zeros((2, 3, 3))
+    D[0] = np.diag([0.5, 2.0, 3.0])  # smallest a00: e0 itself
+    D[1] = np.diag([3.0, 0.5, 2.0])  # smallest a11: (A - l0)(A - l1) e0 = 0
+    v = DO.fast_eigen3x3(D)
+    np.testing.assert_array_equal(v[0], [1.0, 0.0, 0.0])
+    np.testing.assert_array_equal(v[1], [0.0, 0.0, 0.0])
+    # on a noisy plane through the origin with normal along -x the estimate is along +x
+    u = rng.rand(400, 2)
+    p = np.stack([1e-3 * rng.randn(400), u[:, 0], u[:, 1]], 1).astype(np.float32)
+    n, _ = DO.estimate_normals(p, 0.2, 30)
+    assert np.mean(n[:, 0] > 0.99) > 0.95

@@ -120,6 +120,24 @@ def test_pair_stats_match_reference_metrics():
         assert abs(st[b, 6] - p) < 1e-12 and abs(st[b, 7] - r) < 1e-12 and abs(st[b, 8] - f) < 1e-12, b
 
 
+def test_pair_stats_ragged_counts():
+    """Zero-padded labels of a ragged batch: the input inlier ratio divides by each
+    pair's own count; every other column is unchanged by the padding."""
+    rng = np.random.RandomState(3)
+    T = torch.eye(4).expand(3, 4, 4).clone()
+    counts = [50, 80, 120]
+    gl = torch.zeros(3, 120)
+    pl = torch.zeros(3, 120)
+    for b, n in enumerate(counts):
+        gl[b, :n] = torch.from_numpy((rng.rand(n) < 0.3).astype(np.float32))
+        pl[b, :n] = torch.from_numpy((rng.rand(n) < 0.3).astype(np.float32))
+    st = ev.pair_stats(T, T, pl, gl, counts=counts).numpy()
+    for b, n in enumerate(counts):
+        one = ev.pair_stats(T[b:b + 1], T[b:b + 1], pl[b:b + 1, :n], gl[b:b + 1, :n]).numpy()[0]
+        np.testing.assert_allclose(st[b], one, rtol=1e-12)
+    assert ev.pair_sizes(4, (700, 1300)) == ev.pair_sizes(4, (700, 1300)) and ev.pair_sizes(3, 9) == [9, 9, 9]
+
+
 def test_aggregate_scene_then_mean():
     rows = np.zeros((5, 12))
     rows[:, 0] = [1, 0, 1, 1, 1]        # success
@@ -173,3 +191,7 @@ def test_evaluate_synthetic_on_device(gpu_device):
     assert summary["pairs"] == 12
     assert summary["all_pairs"]["success"] >= 0.9  # synthetic pairs with 30 % inliers register
     assert 0.0 <= summary["all_pairs"]["f1"] <= 1.0
+    # mixed sizes: the ragged forward (PointDSC.forward_list's kernel) per batch
+    stats2, summary2 = ev.evaluate_synthetic(m, 12, (500, 900), "3dmatch", batch=5, device=gpu_device)
+    assert stats2.shape == (12, 12) and summary2["all_pairs"]["success"] >= 0.9
+    assert np.all((stats2[:, 4] > 0.2) & (stats2[:, 4] < 0.4))  # input inlier ratio over each pair's own N

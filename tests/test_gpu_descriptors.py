@@ -72,12 +72,17 @@ def test_radius_knn_duplicates_and_sparse(gpu_device):
     assert np.array_equal(d2.cpu().numpy(), rd)
 
 
-def _normal_check(ours, ref, w, pts, vp):
+def _normal_check(ours, ref, w, pts, vp=None):
     """Unit normals equal up to fp32 rounding where the eigenproblem is well posed
-    (smallest eigenvalue separated) and the orientation test is not a tie."""
+    (smallest eigenvalue separated) and the sign is not a near-tie: |n_x| not
+    tiny for open3d's own sign (vp None: FastEigen3x3 gives n_x >= 0), the
+    orientation test not a tie otherwise."""
     ours, ref = ours.astype(np.float64), ref.astype(np.float64)
     gap = (w[:, 1] - w[:, 0]) / np.maximum(w[:, 2], 1e-30)
-    side = np.abs(np.sum(ref * (vp - pts), 1)) / np.maximum(np.linalg.norm(vp - pts, axis=1), 1e-30)
+    if vp is None:
+        side = np.abs(ref[:, 0])
+    else:
+        side = np.abs(np.sum(ref * (vp - pts), 1)) / np.maximum(np.linalg.norm(vp - pts, axis=1), 1e-30)
     ok = (gap > 1e-3) & (side > 1e-4)
     assert ok.mean() > 0.95
     err = np.abs(ours[ok] - ref[ok]).max()
@@ -87,14 +92,21 @@ def _normal_check(ours, ref, w, pts, vp):
 def test_normals_downsampled(gpu_device):
     from pointdsc_amd import descriptors as D
     d = _down(gpu_device)
-    ours = D.estimate_normals(torch.from_numpy(d).to(gpu_device), 2 * V, 30).cpu().numpy()
+    td = torch.from_numpy(d).to(gpu_device)
+    ours = D.estimate_normals(td, 2 * V, 30).cpu().numpy()  # open3d 0.9's sign (the demo's)
     ref, w = DO.estimate_normals(d, 2 * V, 30)
     np.testing.assert_allclose(np.linalg.norm(ours, axis=1), 1.0, atol=1e-6)
-    _normal_check(ours, ref, w, d.astype(np.float64), d.astype(np.float64).mean(0))
+    assert np.all(ours[:, 0] >= 0)
+    _normal_check(ours, ref, w, d.astype(np.float64))
     vp = np.array([0.0, 0.0, 0.0], np.float32)  # an explicit viewpoint (the sensor)
-    ours = D.estimate_normals(torch.from_numpy(d).to(gpu_device), 2 * V, 30, viewpoint=vp).cpu().numpy()
+    ours = D.estimate_normals(td, 2 * V, 30, viewpoint=vp).cpu().numpy()
     ref, w = DO.estimate_normals(d, 2 * V, 30, viewpoint=vp)
     _normal_check(ours, ref, w, d.astype(np.float64), vp.astype(np.float64))
+    ours = D.estimate_normals(td, 2 * V, 30, orient="centroid").cpu().numpy()
+    ref, w = DO.estimate_normals(d, 2 * V, 30, orient="centroid")
+    _normal_check(ours, ref, w, d.astype(np.float64), d.astype(np.float64).mean(0))
+    with pytest.raises(ValueError):
+        D.estimate_normals(td, 2 * V, 30, orient="viewpoint")
 
 
 def test_normals_raw_cloud_subset(gpu_device):
@@ -105,7 +117,7 @@ def test_normals_raw_cloud_subset(gpu_device):
     ours = D.estimate_normals(torch.from_numpy(p).to(gpu_device), 2 * V, 30).cpu().numpy()
     q = np.random.RandomState(0).choice(len(p), 2000, replace=False)
     ref, w = DO.estimate_normals(p, 2 * V, 30, queries=q)
-    _normal_check(ours[q], ref, w, p[q].astype(np.float64), p.astype(np.float64).mean(0))
+    _normal_check(ours[q], ref, w, p[q].astype(np.float64))
 
 
 def test_fpfh_vs_oracle(gpu_device):
@@ -144,16 +156,21 @@ def _pose_error(T, G):
     return re, np.linalg.norm(t - tg) * 100
 
 
-def test_demo_self_registration(gpu_device):
+@pytest.mark.parametrize("orient,max_angle", [("centroid", np.pi), ("open3d", np.pi / 6)])
+def test_demo_self_registration(orient, max_angle, gpu_device):
     """configs[0] on cloud_bin_0 against a known rigid motion of itself: FPFH ->
     NN matching -> PointDSC forward recovers the motion (RE/TE thresholds of
-    libs/loss.py's 3DMatch success: 15 deg / 30 cm; here far tighter)."""
+    libs/loss.py's 3DMatch success: 15 deg / 30 cm; here far tighter).
+    Centroid-oriented normals make FPFH invariant to any rigid motion; with
+    open3d's own sign (n_x >= 0, the demo's default) a normal whose x component
+    changes sign under the motion flips its features, so the rotation is
+    kept moderate there."""
     from pointdsc_amd.demo import RELEASE_3DMATCH, build_model, register
     p = _cloud()
-    G = _rt(7)
+    G = _rt(7, max_angle)
     q = (p.astype(np.float64) @ G[:3, :3].T + G[:3, 3]).astype(np.float32)
     model = build_model(RELEASE_3DMATCH, None, gpu_device)
-    res = register(model, p, q, V, gpu_device)
+    res = register(model, p, q, V, gpu_device, orient=orient)
     T = res["final_trans"].cpu().numpy().astype(np.float64)
     re, te = _pose_error(T, G)
     assert re < 1.0 and te < 3.0, (re, te)
