@@ -11,6 +11,7 @@
 #define PDSC_DEV __device__ __forceinline__
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace pdsc {
