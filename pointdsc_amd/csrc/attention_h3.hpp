@@ -68,6 +68,13 @@ constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by
 #ifndef ATT_SOFTMAX_PRIO
 #define ATT_SOFTMAX_PRIO 1  // s_setprio of the softmax section (build knob; 0 = off)
 #endif
+#ifndef ATT_QFMA
+#define ATT_QFMA 1  // Q pre-scaled by log2(e)/sqrt(C) at production; logits minus the running base by one fma
+#endif
+#ifndef ATT_BUFDMA
+#define ATT_BUFDMA 1  // K/V (and pw2 weight) LDS-DMA by buffer_load ... lds (no per-piece 64-bit address VALU)
+#endif
+constexpr float H3_QSCALE = 0.12751743082459868f;  // log2(e) / sqrt(128): the softmax's scale, in base 2
 constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8 (p * 2^-e stays >= 2^-24 of the sum)
 
 // The V-tile exponent for a tile whose max |v| is vmax: the largest e <= 8 with
@@ -192,6 +199,51 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
     return mfma_h(wh, xh, c);
 }
 
+// Diagnostic build only (-DATT_STAMPS, tools/att_stamps.py): s_memtime stamps of
+// the waves of every 16th workgroup (the first 64 of them) -- per key tile: top,
+// S and M ready, softmax done, PV issued, barrier passed; then the chain phase.
+// Stamps go to a buffer of their own that nothing in the kernel reads.
+#ifdef ATT_STAMPS
+constexpr int ST_PER_WAVE = 192, ST_WGS = 64;
+static __device__ unsigned long long g_att_stamps[ST_WGS * 4 * ST_PER_WAVE];
+PDSC_DEV unsigned long long *att_stamp_ptr(int wave) {
+    return (blockIdx.x % 16 == 0 && blockIdx.x / 16 < ST_WGS && wave < 4)
+               ? g_att_stamps + ((blockIdx.x / 16) * 4 + wave) * ST_PER_WAVE
+               : nullptr;
+}
+#define ATT_STAMP(stp, i)                                                       \
+    do {                                                                        \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+        if (stp) {                                                              \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+            if (lane == 0) stp[i] = t_;                                         \
+        }                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                      \
+    } while (0)
+#define ATT_RSTAMP(stp, i)                                                      \
+    do {                                                                        \
+        if (stp) {                                                              \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();     \
+            if (lane == 0) stp[i] = t_;                                         \
+        }                                                                       \
+    } while (0)
+#define CH_STAMP(i)                                       \
+    do {                                                  \
+        unsigned long long *stc_ = att_stamp_ptr(wave);   \
+        ATT_STAMP(stc_, i);                               \
+    } while (0)
+#else
+#define CH_STAMP(i) \
+    do {            \
+    } while (0)
+#define ATT_STAMP(stp, i) \
+    do {                  \
+    } while (0)
+#define ATT_RSTAMP(stp, i) \
+    do {                   \
+    } while (0)
+#endif
+
 // K/V ring: 2 slots (tile t + 1 lands while tile t is consumed)
 constexpr int H3_NSLOT = 2;
 template <int NW>
@@ -279,16 +331,29 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     }
 
     // LDS-DMA copy of tile st (K 16 KiB + V 16 KiB = 32 pieces of 1 KiB) into ring slot `slot`
+#if ATT_BUFDMA
+    const __amdgpu_buffer_rsrc_t rK = h3_rsrc(Kp, (uint32_t)Npad * H3_ROWB), rV = h3_rsrc(Vp, (uint32_t)Npad * H3_ROWB);
+#endif
     auto stage = [&](int st, int slot) {
         char *dst = h3smem + slot * (H3_KTB + H3_VTB);
         constexpr int PIECES = (H3_KTB + H3_VTB) / 1024;
 #pragma unroll
         for (int i = 0; i < PIECES / NW; ++i) {
-            const int piece = wave * (PIECES / NW) + i;
+            const int piece = wave * (PIECES / NW) + i;  // wave-uniform (SGPR)
+#if ATT_BUFDMA
+            // the piece's offset in the SGPR operand: no per-piece address VALU
+            if (piece < H3_KTB / 1024)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rK, (__attribute__((address_space(3))) void *)(dst + piece * 1024),
+                                                         16, 16 * lane, st * H3_KTB + piece * 1024, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rV, (__attribute__((address_space(3))) void *)(dst + piece * 1024),
+                                                         16, 16 * lane, st * H3_VTB + (piece - H3_KTB / 1024) * 1024, 0, 0);
+#else
             const char *src = piece < H3_KTB / 1024
                                   ? Kp + (size_t)st * H3_KTB + piece * 1024
                                   : Vp + (size_t)st * H3_VTB + (piece - H3_KTB / 1024) * 1024;
             __builtin_amdgcn_global_load_lds(src + 16 * lane, dst + piece * 1024, 16, 0, 0);
+#endif
         }
     };
 
@@ -296,9 +361,14 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     for (int t = 0; t < 4; ++t) O[t] = zero16();
     m_run = -INFINITY;
     l_run = 0.0f;
-    const float scale = 0.12751743082459868f;  // log2(e) / sqrt(128)
+    const float scale = ATT_QFMA ? 1.0f : H3_QSCALE;  // (QFMA: Q carries it)
     const uint32_t Nb = (uint32_t)g.N * 4;
 
+#ifdef ATT_STAMPS
+    unsigned long long *stp = att_stamp_ptr(wave);
+#endif
+    int st_si = 0;  // the current tile's first stamp index (diagnostic build)
+    (void)st_si;
     const float *vexp_b = vexp + (size_t)b * (Npad / H3_TILE);
     const __amdgpu_buffer_rsrc_t rE = h3_rsrc(vexp_b, (uint32_t)(Npad / H3_TILE) * 4u);
     // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys of tile key0
@@ -348,7 +418,8 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // (the tile's V exponent is a vector load issued with the M loads: a scalar
     // load here is waited for with lgkmcnt(0) in the middle of the softmax)
     // QK^T + online softmax of one key tile -> this lane's P fragments (ph, pl)
-    auto qk_softmax = [&](const char *Kl, int key0, float (&mv)[16], float ev, f16x8(&ph)[2], f16x8(&pl)[2]) {
+    auto qk_softmax = [&](const char *Kl, int key0, float (&mv)[16], float ev, f16x8(&ph)[2], f16x8(&pl)[2],
+                          bool first) {
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
         f16x8 kf[3][2];
@@ -369,32 +440,72 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         if (ATT_SOFTMAX_PRIO > 0) __builtin_amdgcn_s_setprio(ATT_SOFTMAX_PRIO);
         float p[16];
         float mx = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = mv[r] * (S[r] * scale);  // (:39) then * M (:41); 0, not -inf, off-support
-        if (key0 + 32 > N) {  // wave-uniform: only the last key tile has padding keys
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (key0 + acc_row(r, h) >= N) p[r] = -INFINITY;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, p[r]);
-        mx = halves_max(mx);
-        if (__any(mx > m_run + H3_DEFER)) {  // wave-uniform re-base of the running max
-            const float m_new = fmaxf(m_run, mx);
-            const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-            m_run = m_new;
-            l_run *= alpha;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) O[t][r] *= alpha;  // lane = query
-        }
-        const float mb = m_run - (float)H3_PSHIFT + ev;
-        float psum = 0.0f;
+        // p = the exponent of this tile's softmax weights relative to the base
+        // mb = m_run - PSHIFT + ev (log2 units); the running max m_run is
+        // re-based (lazily) when the tile's max exceeds it by > DEFER.
         float ex[16];
+        if (ATT_QFMA && !first) {  // wave-uniform (scalar): every tile but the first (m_run = -inf there)
+            // logit * M - mb in one rounding (Q carries log2(e)/sqrt(C), :39 and :41)
+            const float mb0 = m_run - (float)H3_PSHIFT + ev;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[r] = __builtin_fmaf(mv[r], S[r], -mb0);
+            ATT_STAMP(stp, st_si + 1);
+            ATT_STAMP(stp, st_si + 2);
+            if (key0 + 32 > N) {  // wave-uniform: only the last key tile has padding keys
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (key0 + acc_row(r, h) >= N) p[r] = -INFINITY;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, p[r]);
+            mx = halves_max(mx);
+            // logit max > m_run + DEFER  <=>  mx > DEFER + PSHIFT - ev
+            if (__any(mx > H3_DEFER + (float)H3_PSHIFT - ev)) {
+                const float m_new = fmaxf(m_run, mx + mb0);
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                const float dm = m_new - m_run;
+                m_run = m_new;
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) O[t][r] *= alpha;  // lane = query
+#pragma unroll
+                for (int r = 0; r < 16; ++r) p[r] -= dm;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[r] = S[r] * scale;  // (:39)
+            ATT_STAMP(stp, st_si + 1);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[r] = mv[r] * p[r];  // then * M (:41); 0, not -inf, off-support
+            ATT_STAMP(stp, st_si + 2);
+            if (key0 + 32 > N) {  // wave-uniform: only the last key tile has padding keys
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (key0 + acc_row(r, h) >= N) p[r] = -INFINITY;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, p[r]);
+            mx = halves_max(mx);
+            if (__any(mx > m_run + H3_DEFER)) {  // wave-uniform re-base of the running max
+                const float m_new = fmaxf(m_run, mx);
+                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+                m_run = m_new;
+                l_run *= alpha;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) O[t][r] *= alpha;  // lane = query
+            }
+            const float mb = m_run - (float)H3_PSHIFT + ev;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[r] -= mb;
+        }
+        float psum = 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            ex[r] = __builtin_amdgcn_exp2f(p[r] - mb);
+            ex[r] = __builtin_amdgcn_exp2f(p[r]);
             psum += ex[r];
         }
 #pragma unroll
@@ -448,12 +559,18 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     for (int st = st0; st < st1; ++st) {
         float mv[16], ev;
         f16x8 ph[2], pl[2];
+        const int si = 1 + 6 * min(st - st0, 23);
+        st_si = si;
+        ATT_STAMP(stp, si);
         load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
         if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
         // padding waves (q0 >= Npad) compute on clamped operands and store nothing
-        qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl);
+        qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl, st == st0);
+        ATT_STAMP(stp, si + 3);
         pv(slot_base(st) + H3_KTB, ph, pl);
+        ATT_STAMP(stp, si + 4);
         sync();
+        ATT_STAMP(stp, si + 5);
     }
     l_run = halves_sum(l_run);
 }
@@ -523,7 +640,7 @@ static __global__ void split_qkv_kernel(const float *__restrict__ q, const float
     const size_t src = ((size_t)b * ld + row) * CH + c, pb = (size_t)b * Npad * 2 * CH;
     const bool in = row < N;
     _Float16 hi, lo;
-    split_h(in ? q[src] : 0.0f, hi, lo);
+    split_h(in ? (ATT_QFMA ? q[src] * H3_QSCALE : q[src]) : 0.0f, hi, lo);
     Qs[pb + qs_off(row, 0, c)] = hi;
     Qs[pb + qs_off(row, 1, c)] = lo;
     split_h(in ? k[src] : 0.0f, hi, lo);

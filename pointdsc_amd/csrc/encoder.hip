@@ -501,7 +501,8 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     _Float16 a, b;
-                    split_h(acc[i][8 * s + e] * inv + bias[8 * s + e], a, b);
+                    const float y = acc[i][8 * s + e] * inv + bias[8 * s + e];
+                    split_h(MODE == SPLIT_Q && ATT_QFMA ? y * H3_QSCALE : y, a, b);
                     hi[e] = a;
                     lo[e] = b;
                 }
@@ -809,9 +810,17 @@ static void w2_sched_add(W2Sched &S, const DenseOff &o, int in, int out) {
 // one wave instruction, lane-linear on both sides.
 PDSC_DEV void w2_stage(const float *pk, const W2Sched &S, int c, char *slot, int wave, int lane) {
     if (c >= S.n) return;
+#if ATT_BUFDMA
+    // the piece's offset in the SGPR operand: no per-piece address VALU
+    const __amdgpu_buffer_rsrc_t r = h3_rsrc(pk, 0xFFFFFFFFu);
+    for (int i = wave; i < S.np[c]; i += PW2_W)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)(slot + 1024 * i), 16,
+                                                 16 * lane, (int)(2 * S.off[c]) + 1024 * i, 0, 0);
+#else
     const _Float16 *src = reinterpret_cast<const _Float16 *>(pk) + S.off[c] + 8 * lane;
     for (int i = wave; i < S.np[c]; i += PW2_W)
         __builtin_amdgcn_global_load_lds(src + 512 * i, slot + 1024 * i, 16, 0, 0);
+#endif
 }
 
 struct W2Pipe {
@@ -1003,6 +1012,7 @@ PDSC_DEV void w2_store_row(float *__restrict__ featL, int row, int lane, const f
 // Q / K outputs (transposed, bias only) in the attention_h3 fragment-block
 // tiling: registers 8u .. 8u+7 of tile t = fragment 2t + u of this lane (qk_pos
 // positions 32t + 16u + 8h .. +7 of its point): 16 coalesced 1-KiB stores.
+template <bool QSCALE>  // Q: times log2(e)/sqrt(C) (ATT_QFMA: the attention's softmax scale)
 PDSC_DEV void w2_store_qk(const f32x16 (&acc)[4], float inv, const float *bias, _Float16 *__restrict__ dst, int row,
                           int lane) {
     const int h = lane >> 5;
@@ -1015,7 +1025,10 @@ PDSC_DEV void w2_store_qk(const f32x16 (&acc)[4], float inv, const float *bias, 
             const f32x4 b0 = *reinterpret_cast<const f32x4 *>(bias + c0), b1 = *reinterpret_cast<const f32x4 *>(bias + c0 + 8);
             float v[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(acc[t][8 * u + e], inv, e < 4 ? b0[e] : b1[e - 4]);
+            for (int e = 0; e < 8; ++e) {
+                v[e] = __builtin_fmaf(acc[t][8 * u + e], inv, e < 4 ? b0[e] : b1[e - 4]);
+                if (QSCALE && ATT_QFMA) v[e] *= H3_QSCALE;
+            }
             f16x8 hi, lo;
             split8v(v, hi, lo);
             *reinterpret_cast<f16x8 *>(dtile + h3_frag(2 * t + u, 0, lane)) = hi;
@@ -1085,12 +1098,16 @@ PDSC_DEV void w2_pcn_qkv(W2Pipe &P, const float *__restrict__ pk, const W2Sched 
         w2_epilogue<CH, EPI_BN_RELU>(acc, sp, cf + W2CoefQKV::pcn, nullptr, yh, yl, lane);
         w2_store_row(featL, row, lane, acc);
     }
+    CH_STAMP(175);
     w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
-    if (active) w2_store_qk(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
+    if (active) w2_store_qk<true>(acc, sq, cf + W2CoefQKV::q, Q, row, lane);
+    CH_STAMP(176);
     w2_layer<CH, CH, true, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
-    if (active) w2_store_qk(acc, sk, cf + W2CoefQKV::k, K, row, lane);
+    if (active) w2_store_qk<false>(acc, sk, cf + W2CoefQKV::k, K, row, lane);
+    CH_STAMP(177);
     w2_layer<CH, CH, false, 16>(P, pk, S, yh, yl, acc, active, wave, lane);
     if (active) w2_store_v(acc, sv, cf + W2CoefQKV::v, V + (size_t)(row >> 5) * H3_TILE_H, vexp + (row >> 5), lane);
+    CH_STAMP(178);
 }
 
 // Coefficients of combine + fc_message + PointCN + QKV (pw2_mid / attn_pw2).
@@ -1115,13 +1132,16 @@ PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sche
     f16x8 yh[8], yl[8];
     w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
     if (active) w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc0.scale], cf + W2CoefMid::f0, nullptr, yh, yl, lane);
+    CH_STAMP(172);
     w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + W2CoefMid::f3, nullptr, xh, xl, lane);
         w2_load_row(featL, row, lane, res);  // the residual: lands during fc6's MFMAs
     }
+    CH_STAMP(173);
     w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
     if (active) w2_epilogue<CH, EPI_RESID>(a4, pk[m.fc6.scale], cf + W2CoefMid::f6, res, yh, yl, lane);
+    CH_STAMP(174);
     w2_pcn_qkv(P, pk, S, cf, d, yh, yl, featL, Q, K, V, vexp, row, active, wave, lane);
 }
 
@@ -1201,6 +1221,9 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const floa
 // buffers (Q, K, V, vexp): other workgroups of the pair still read layer l.
 // Bit-identical to attention_h3_kernel + pw2_mid_kernel (a one-split combine
 // is O * (1 / l) exactly).  LDS: the K/V ring, then the weight ring.
+#ifdef DIAG_CFIRST
+static __device__ unsigned g_cu_ctr[16 * 256];
+#endif
 template <bool PACKED>
 __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
@@ -1215,9 +1238,50 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     const int row = blk.qb * PW2_PTS + wave * 32 + (lane & 31);
     const bool active = blk.qb * PW2_PTS + wave * 32 < Npad;  // wave-uniform
     const size_t boff = (size_t)b * Npad * CH;
+#ifdef ATT_STAMPS
+    unsigned long long *stp = att_stamp_ptr(wave);
+    ATT_RSTAMP(stp, 188);
+    ATT_STAMP(stp, 0);
+#endif
+#ifdef DIAG_CFIRST
+    // timing-only diagnostic (wrong results): the second workgroup to arrive on
+    // a CU runs its chain phase (on zero messages) BEFORE its attention, so the
+    // two workgroups of a CU pair attention with chain instead of running the
+    // same phase together.  CU identity from HW_ID (CU, SH, SE) and XCC_ID.
+    {
+        __shared__ unsigned cfirst_sh;
+        if (tid == 0) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);
+            const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+            cfirst_sh = atomicAdd(&g_cu_ctr[(xcc & 15) * 256 + (hw & 255)], 1u) & 1u;
+        }
+        __syncthreads();
+        if (cfirst_sh) {
+            W2Pipe P0{w2smem, 0};
+            float *cf0 = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
+            for (int c = 0; c < PW2_NSLOT; ++c) w2_stage(pk, S, c, P0.slot(c), wave, lane);
+            w2_coef_mid(cf0, pk, m, d, tid);
+            f16x8 zh[8], zl[8];
+            for (int i = 0; i < 8; ++i) zh[i] = zl[i] = f16x8{};
+            __syncthreads();
+            w2_mid_chain(P0, pk, S, cf0, m, d, zh, zl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                         vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+            __syncthreads();
+            ATT_STAMP(stp, 179);
+            f32x16 O0[4];
+            float m0, l0;
+            attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O0, m0, l0);
+            if (active && l0 < 0.0f) featL[0] = O0[0][0] + m0;  // never true: keeps the core live
+            ATT_STAMP(stp, 181);
+            ATT_RSTAMP(stp, 189);
+            return;
+        }
+    }
+#endif
     f32x16 O[4];
     float m_run, l_run;
     attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
+    ATT_STAMP(stp, 170);
     // the K/V ring is free (the core ends on a barrier): weight chunks 0, 1 and the coefficients
     W2Pipe P{w2smem, 0};
     float *cf = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
@@ -1226,9 +1290,24 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     f16x8 xh[8], xl[8];
     if (active) w2_msg_frags(O, l_run, xh, xl);  // msg = O / l
     __syncthreads();
+    ATT_STAMP(stp, 171);
     w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                  vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+    ATT_STAMP(stp, 180);
+    ATT_RSTAMP(stp, 189);
 }
+
+#ifdef ATT_STAMPS
+extern "C" int pdsc_diag_att_stamps(void *host, size_t bytes) {
+    const size_t n = std::min(bytes, sizeof(g_att_stamps));
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int pdsc_diag_att_stamps_clear() {
+    static unsigned long long zero[ST_WGS * 4 * ST_PER_WAVE];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_att_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess ? 0
+                                                                                                             : -1;
+}
+#endif
 
 // Coefficients of the last layer's fc_message + classifier (pw2_last / attn_pw2_last).
 struct W2CoefLast {
