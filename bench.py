@@ -13,12 +13,14 @@ Prints ONE JSON line (rank 0).  Also measured live with HIP events on the
 stream the kernels run on:
   roofline      -- the dominant kernel (SCNonlocal attention), MFMA bound; its fp32
                    products run as 3 fp16 MFMAs, so the peak is 2500/3 TFLOP/s
-  roofline_hbm  -- the a1 compatibility kernel, HBM-write bound
+  roofline_hbm  -- the forward's a1 compatibility kernel (symmetric-packed M), HBM-write bound;
+                   roofline_hbm_dense: the dense-M form
   roofline_path -- SURVEY 8(d)'s target: the compat + seed-kNN + NSM power-iteration
                    stages at N=5000 (stage events inside the forward), HBM bound,
                    priced with the algorithmic bytes B(N) = 24N + 4N^2 + S*k*(C+6)*4 + 4*S*k
   stages        -- per-stage ms of the headline forward (pdsc_forward_timing events)
-  roofline_sm   -- SURVEY 8(f) row 3: the SM baseline's matrix-vector product at N=5000, HBM bound
+  roofline_sm   -- SURVEY 8(f) row 3: the SM baseline's matrix-vector product at N=9000 (M past the
+                   Infinity Cache), HBM bound
   single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph
   ragged        -- one call over P pairs of mixed N (0.7-1.3 N), the evaluation loop's shape
 Each roofline's `traffic` is the HBM bytes per launch of the same kernel at the
@@ -377,8 +379,31 @@ def main():
                     "launch_ms": round(att_ms, 4), "launches_timed": len(att_times),
                     "flop_per_launch": flops, "share_of_step": round(n_launch * att_ms / ms_per_step, 3)}
         sp = ctypes.c_void_p(stream.cuda_stream)
-        Mo = torch.empty((P, N, N), dtype=torch.float32, device=dev)
         sd = model.sigma_spat.detach()
+        ntile = (N + 63) // 64
+        # the forward's a1 kernel: M written once as the symmetric-packed 32 x 32 tiles
+        # (pdsc_compat_packed_f32), priced on the bytes it moves (packed M out + 24 N in)
+        nfp = L.pdsc_compat_packed_floats(N)
+        Mp = torch.empty((P, nfp), dtype=torch.float32, device=dev)
+
+        def comp_p():
+            L.pdsc_compat_packed_f32(src.data_ptr(), tgt.data_ptr(), P, N, sd.data_ptr(), Mp.data_ptr(), sp)
+
+        cp_ms = event_time(comp_p, args.kernel_iters, stream)
+        cpbytes = P * (4.0 * nfp + 24.0 * N)
+        cpach = cpbytes / (cp_ms * 1e-3) / 1e9
+        cp_prof = profiled("compat_packed_kernel", ntile * (ntile + 1) // 2 * P * 256)
+        roofline_hbm = {"kernel": "compat_packed_kernel (the forward's a1)", "bound": "hbm",
+                        "achieved": round(cpach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(cpach / PEAK_HBM_GBS, 4),
+                        "traffic": cp_prof and cp_prof["hbm_bytes"], "profile": cp_prof,
+                        "launch_ms": round(cp_ms, 4), "bytes_per_launch": cpbytes,
+                        "dense_equivalent_GBs": round(P * (4.0 * N * N + 24.0 * N) / (cp_ms * 1e-3) / 1e9, 1),
+                        "note": "bytes = the packed upper-triangle tiles written (about 2 N^2 per pair) + 24 N read; "
+                                "dense_equivalent prices the same launch at the reference's dense 4 N^2"}
+        del Mp
+        # the dense form (pdsc_compat_f32: the exact-fp32 forward and the standalone API)
+        Mo = torch.empty((P, N, N), dtype=torch.float32, device=dev)
 
         def comp():
             L.pdsc_compat_f32(src.data_ptr(), tgt.data_ptr(), P, N, sd.data_ptr(), Mo.data_ptr(), sp)
@@ -386,12 +411,12 @@ def main():
         c_ms = event_time(comp, args.kernel_iters, stream)
         cbytes = P * (4.0 * N * N + 24.0 * N)
         cach = cbytes / (c_ms * 1e-3) / 1e9
-        ntile = (N + 63) // 64
         c_prof = profiled("compat_kernel", ntile * (ntile + 1) // 2 * P * 256)
-        roofline_hbm = {"kernel": "compat_kernel", "bound": "hbm", "achieved": round(cach, 1),
-                        "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(cach / PEAK_HBM_GBS, 4),
-                        "traffic": c_prof and c_prof["hbm_bytes"], "profile": c_prof,
-                        "launch_ms": round(c_ms, 4), "bytes_per_launch": cbytes}
+        roofline_hbm_dense = {"kernel": "compat_kernel (dense M)", "bound": "hbm", "achieved": round(cach, 1),
+                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(cach / PEAK_HBM_GBS, 4),
+                              "traffic": c_prof and c_prof["hbm_bytes"], "profile": c_prof,
+                              "launch_ms": round(c_ms, 4), "bytes_per_launch": cbytes}
+        del Mo
 
         stage_ms, _ = sev.stage_means()
         stages = {k: round(v, 4) for k, v in stage_ms.items()}
@@ -448,21 +473,25 @@ def main():
         roofline_sm = None
         if args.path_n > 0:
             from pointdsc_amd.baselines import SM, sm_matvec
+            # the matrix-vector product at N = 9000: M = 324 MB, past the 256 MB Infinity
+            # Cache, so each product streams M from HBM; the whole SM call at N = path_n
             Ns = args.path_n
-            Mm = torch.rand((Ns, Ns), dtype=torch.float32, device=dev)
-            vv = torch.rand(Ns, dtype=torch.float32, device=dev)
+            Nmv = max(Ns, 9000)
+            Mm = torch.rand((Nmv, Nmv), dtype=torch.float32, device=dev)
+            vv = torch.rand(Nmv, dtype=torch.float32, device=dev)
             mv_ms = event_time(lambda: sm_matvec(Mm, vv), 50, stream)
-            mvb = 4.0 * Ns * Ns + 8.0 * Ns
+            mvb = 4.0 * Nmv * Nmv + 8.0 * Nmv
             d1s = synthetic_batch(1, Ns, seed=9000 + rank, preset=args.preset)
             cs, ss, ts = (torch.from_numpy(d1s[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
             sm_ms = event_time(lambda: SM(cs, ss, ts, inlier_threshold=p["inlier_threshold"]), 5, stream)
-            mv_prof = profiled("sm_matvec_kernel", (Ns + 3) // 4 * 256)
-            roofline_sm = {"kernel": "sm_matvec_kernel", "bound": "hbm", "num_corr": Ns,
+            mv_prof = profiled("sm_matvec_kernel", (Nmv + 3) // 4 * 256)
+            roofline_sm = {"kernel": "sm_matvec_kernel", "bound": "hbm", "num_corr": Nmv, "sm_num_corr": Ns,
                            "traffic": mv_prof and mv_prof["hbm_bytes"], "profile": mv_prof,
                            "achieved": round(mvb / (mv_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                            "frac": round(mvb / (mv_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4), "launch_ms": round(mv_ms, 4),
                            "bytes_per_launch": mvb,
-                           "note": "M (100 MB at N=5000) can sit in the 256 MB Infinity Cache between iterates",
+                           "note": f"M ({4 * Nmv * Nmv / 1e6:.0f} MB) exceeds the 256 MB Infinity Cache: "
+                                   "every product streams it from HBM",
                            "sm_pair_ms": round(sm_ms, 3)}
             del Mm, vv
 
@@ -573,7 +602,8 @@ def main():
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
-            "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_path": roofline_path,
+            "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_hbm_dense": roofline_hbm_dense,
+            "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
             "stages_ms": stages, "single_pair": single, "ragged": ragged, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
         }

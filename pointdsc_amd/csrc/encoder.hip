@@ -1221,9 +1221,6 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const floa
 // buffers (Q, K, V, vexp): other workgroups of the pair still read layer l.
 // Bit-identical to attention_h3_kernel + pw2_mid_kernel (a one-split combine
 // is O * (1 / l) exactly).  LDS: the K/V ring, then the weight ring.
-#ifdef DIAG_CFIRST
-static __device__ unsigned g_cu_ctr[16 * 256];
-#endif
 template <bool PACKED>
 __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
@@ -1242,41 +1239,6 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     unsigned long long *stp = att_stamp_ptr(wave);
     ATT_RSTAMP(stp, 188);
     ATT_STAMP(stp, 0);
-#endif
-#ifdef DIAG_CFIRST
-    // timing-only diagnostic (wrong results): the second workgroup to arrive on
-    // a CU runs its chain phase (on zero messages) BEFORE its attention, so the
-    // two workgroups of a CU pair attention with chain instead of running the
-    // same phase together.  CU identity from HW_ID (CU, SH, SE) and XCC_ID.
-    {
-        __shared__ unsigned cfirst_sh;
-        if (tid == 0) {
-            const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);
-            const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
-            cfirst_sh = atomicAdd(&g_cu_ctr[(xcc & 15) * 256 + (hw & 255)], 1u) & 1u;
-        }
-        __syncthreads();
-        if (cfirst_sh) {
-            W2Pipe P0{w2smem, 0};
-            float *cf0 = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
-            for (int c = 0; c < PW2_NSLOT; ++c) w2_stage(pk, S, c, P0.slot(c), wave, lane);
-            w2_coef_mid(cf0, pk, m, d, tid);
-            f16x8 zh[8], zl[8];
-            for (int i = 0; i < 8; ++i) zh[i] = zl[i] = f16x8{};
-            __syncthreads();
-            w2_mid_chain(P0, pk, S, cf0, m, d, zh, zl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                         vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
-            __syncthreads();
-            ATT_STAMP(stp, 179);
-            f32x16 O0[4];
-            float m0, l0;
-            attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O0, m0, l0);
-            if (active && l0 < 0.0f) featL[0] = O0[0][0] + m0;  // never true: keeps the core live
-            ATT_STAMP(stp, 181);
-            ATT_RSTAMP(stp, 189);
-            return;
-        }
-    }
 #endif
     f32x16 O[4];
     float m_run, l_run;
