@@ -80,10 +80,24 @@ int check_cfg(const pdsc_config *cfg) {
     return PDSC_OK;
 }
 
+// The tiniest batches (<= 16 query blocks of 128, >= 16 key splits: a single
+// N = 1000 pair) combine the attention partials in their own launch
+// (combine_rows) rather than in the pointwise kernel's prologue: measured
+// 0.511 -> 0.482 ms per single-pair forward, but slower from 4 pairs of
+// N = 1000 on (an extra launch per layer).  A/B knob PDSC_PRECOMBINE=0 (never).
+static bool use_precombine(int B, int Npad, int nsplit, bool f32, bool fuse) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_PRECOMBINE");
+        return e && e[0] == '0';
+    }();
+    return !off && !f32 && !fuse && nsplit >= 16 && (long)B * (Npad / QB) <= 16;
+}
+
 struct Dims {
     int B, N, Npad, S, k, T, nsplit;
     bool f32;   // PDSC_PRECISION_F32
     bool fuse;  // attention + pointwise chain in one launch per layer (attention_fused)
+    bool precombine;  // split partials combined by combine_rows ahead of the pointwise kernels
 };
 
 int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
@@ -98,6 +112,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     d.f32 = cfg->precision == PDSC_PRECISION_F32;
     d.nsplit = attention_nsplit(B, N, d.f32);
     d.fuse = attention_fused(B, N, d.f32);
+    d.precombine = use_precombine(B, d.Npad, d.nsplit, d.f32, d.fuse);
     if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
     if (d.k > 63) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 63", d.k);
     return PDSC_OK;
@@ -107,6 +122,7 @@ struct EncBufs {
     float *feat, *opart, *ml, *vexp, *vexp2;
     _Float16 *q, *k, *v;     // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
     _Float16 *q2, *k2, *v2;  // the other Q/K/V set of the fused path (layers alternate), else null
+    float *opart1, *ml1;     // the combined split (Dims::precombine), else null
 };
 
 EncBufs carve_encoder(Carve &c, const Dims &d) {
@@ -119,6 +135,8 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
     e.opart = c.take<float>(rows * d.nsplit);
     e.ml = c.take<float>((size_t)d.B * d.Npad * d.nsplit * 2);
     e.vexp = c.take<float>((size_t)d.B * (d.Npad / 32));
+    e.opart1 = d.precombine ? c.take<float>(rows) : nullptr;
+    e.ml1 = d.precombine ? c.take<float>((size_t)d.B * d.Npad * 2) : nullptr;
     e.q2 = e.k2 = e.v2 = nullptr;
     e.vexp2 = nullptr;
     if (d.fuse) {
@@ -158,12 +176,20 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
         HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
                                 s, rg));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
+        const float *op = e.opart, *mlp = e.ml;
+        int ns = d.nsplit;
+        if (d.precombine) {
+            HIPCHK(launch_combine_rows(e.opart, e.ml, d.B, d.Npad, d.nsplit, e.opart1, e.ml1, s));
+            op = e.opart1;
+            mlp = e.ml1;
+            ns = 1;
+        }
         if (l + 1 < lay.L)
-            HIPCHK(launch_pw_mid(packed, lay, l, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat, e.q,
-                                 e.k, e.v, e.vexp, s));
+            HIPCHK(launch_pw_mid(packed, lay, l, d.f32, op, mlp, ns, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp,
+                                 s));
         else
-            HIPCHK(launch_pw_last(packed, lay, d.f32, e.opart, e.ml, d.nsplit, d.B, d.N, d.Npad, e.feat,
-                                  feat_out, normed, d.f32 ? nullptr : normed_s, conf, s));
+            HIPCHK(launch_pw_last(packed, lay, d.f32, op, mlp, ns, d.B, d.N, d.Npad, e.feat, feat_out, normed,
+                                  d.f32 ? nullptr : normed_s, conf, s));
     }
     return PDSC_OK;
 }

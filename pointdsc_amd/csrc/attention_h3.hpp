@@ -588,9 +588,16 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     // barrier's count) is then a scalar branch, never an exec-masked one
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5;
     const int q0 = blk.qb * (NW * 32) + wave * 32, qq = q0 + (lane & 31);
+#ifdef ATT_STAMPS
+    unsigned long long *stp = att_stamp_ptr(wave);
+    ATT_RSTAMP(stp, 184);
+    ATT_STAMP(stp, 160);
+#endif
     f32x16 O[4];
     float m_run, l_run;
     attention_h3_core<NW, PACKED>(Qs, Ks, Vs, vexp, M, g, blk, h3smem, wave, lane, O, m_run, l_run);
+    ATT_STAMP(stp, 161);
+    ATT_RSTAMP(stp, 185);
     if (q0 >= Npad) return;
     const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
     // registers 8u + 4g .. +3 of tile t = fragment block 2 (2t + u) + g (16 coalesced 1-KiB stores)

@@ -279,6 +279,70 @@ hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, in
     return hipGetLastError();
 }
 
+// Small batches (many key splits): the split partials combined ahead of the
+// pointwise kernel by 32 threads per row (4 channels each), every split's
+// loads of a 16-split chunk issued together -- one L2 round trip per chunk
+// where combine16 (8 threads per row, 16 channels) needs six for 16 splits --
+// and written back as ONE split (m = 0, l = 1) that the pointwise kernel's
+// combine16 reads unchanged (w = e^0 = 1, L = 1 l = 1, acc = 1 O, O / 1).  The
+// same operations in the same order per channel as combine16: bit-identical.
+constexpr int CMB_SB = 16;
+__global__ __launch_bounds__(256) void combine_rows_kernel(const float *__restrict__ opart,
+                                                           const float *__restrict__ ml, int nsplit, int Npad,
+                                                           float *__restrict__ opart1, float *__restrict__ ml1) {
+    const int b = blockIdx.y, row = blockIdx.x * 8 + (threadIdx.x >> 5), d0 = 4 * (threadIdx.x & 31);
+    if (row >= Npad) return;
+    const float *mlb = ml + ((size_t)b * nsplit * Npad + row) * 2;  // split s: mlb[s * Npad * 2 + {0, 1}]
+    const size_t oo = h3_opart_off(row, d0);
+    float mstar = -INFINITY;
+    if (nsplit > CMB_SB) {  // the maxima first when they do not fit one chunk
+        for (int s0 = 0; s0 < nsplit; s0 += CMB_SB) {
+            float mv[CMB_SB];
+#pragma unroll
+            for (int j = 0; j < CMB_SB; ++j) mv[j] = s0 + j < nsplit ? mlb[(size_t)(s0 + j) * Npad * 2] : -INFINITY;
+#pragma unroll
+            for (int j = 0; j < CMB_SB; ++j) mstar = fmaxf(mstar, mv[j]);
+        }
+    }
+    float L = 0.0f;
+    f32x4 acc = {};
+    for (int s0 = 0; s0 < nsplit; s0 += CMB_SB) {
+        f32x2 mlv[CMB_SB];
+        f32x4 ov[CMB_SB];
+#pragma unroll
+        for (int j = 0; j < CMB_SB; ++j) {
+            if (s0 + j < nsplit) {
+                const size_t base = (size_t)(b * nsplit + s0 + j) * Npad;
+                mlv[j] = *reinterpret_cast<const f32x2 *>(ml + (base + row) * 2);
+                ov[j] = *reinterpret_cast<const f32x4 *>(opart + base * CH + oo);
+            }
+        }
+        if (nsplit <= CMB_SB) {
+#pragma unroll
+            for (int j = 0; j < CMB_SB; ++j)
+                if (j < nsplit) mstar = fmaxf(mstar, mlv[j][0]);
+        }
+#pragma unroll
+        for (int j = 0; j < CMB_SB; ++j) {
+            if (s0 + j < nsplit) {
+                const float w = expf(mlv[j][0] - mstar);
+                L += w * mlv[j][1];
+                acc += w * ov[j];
+            }
+        }
+    }
+    const size_t base1 = (size_t)b * Npad;
+    *reinterpret_cast<f32x4 *>(opart1 + base1 * CH + oo) = f32x4{acc[0] / L, acc[1] / L, acc[2] / L, acc[3] / L};
+    if (d0 == 0) *reinterpret_cast<f32x2 *>(ml1 + (base1 + row) * 2) = f32x2{0.0f, 1.0f};
+}
+
+hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int Npad, int nsplit, float *opart1,
+                               float *ml1, hipStream_t s) {
+    hipLaunchKernelGGL(combine_rows_kernel, dim3((Npad + 7) / 8, B), dim3(256), 0, s, opart, ml, nsplit, Npad, opart1,
+                       ml1);
+    return hipGetLastError();
+}
+
 // ============================================================ pointwise chain
 // A workgroup (4 waves) owns PT = 64 points (two 32-row MFMA tiles) held in LDS
 // and runs the whole per-point chain between two attention launches.
@@ -567,6 +631,7 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
     asm volatile("" ::: "memory");
     dense_tile_w<CH, CH, EPI_BN_RELU, PTT / 32, F32>(Xin, S132, pa, pk, d.pcn, 0, wave, Xout, S132, nullptr, lane);
     __syncthreads();  // Xout complete; Xin is dead (H3: it now holds the split copy of Xout)
+    CH_STAMP(155);
     if constexpr (F32) {
         float *Qf = reinterpret_cast<float *>(Q) + (size_t)p0 * CH, *Kf = reinterpret_cast<float *>(K) + (size_t)p0 * CH,
               *Vf = reinterpret_cast<float *>(V) + (size_t)p0 * CH;
@@ -585,11 +650,15 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
         asm volatile("" ::: "memory");
         store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
         __syncthreads();
+        CH_STAMP(156);
         dense_split<SPLIT_Q, PTT / 32>(Xs, pb, pk, d.q, wave, Q, p0, lane);
         load_wpanel<CH, CH, F32>(pk, d.v, wave, lane, pb);
         asm volatile("" ::: "memory");
+        CH_STAMP(157);
         dense_split<SPLIT_K, PTT / 32>(Xs, pa, pk, d.k, wave, K, p0, lane);
+        CH_STAMP(158);
         dense_split<SPLIT_V, PTT / 32>(Xs, pb, pk, d.v, wave, V, p0, lane, Xout, vexp);  // Xout is dead
+        CH_STAMP(159);
     }
 }
 
@@ -656,10 +725,13 @@ PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restric
                             const float *__restrict__ feat_rows, int wave, int lane) {
     dense64<CH, CH2, EPI_BN_RELU, PTT, F32>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
     __syncthreads();
+    CH_STAMP(152);
     dense64<CH2, CH2, EPI_BN_RELU, PTT, F32>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
     __syncthreads();
+    CH_STAMP(153);
     dense64<CH2, CH, EPI_RESID, PTT, F32>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
     __syncthreads();
+    CH_STAMP(154);
 }
 
 template <int PTT, bool F32>
@@ -674,11 +746,18 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const size_t boff = (size_t)b * Npad * CH;
+#ifdef ATT_STAMPS
+    unsigned long long *stp = att_stamp_ptr(wave);
+    ATT_RSTAMP(stp, 186);
+    ATT_STAMP(stp, 150);
+#endif
     combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
+    ATT_STAMP(stp, 151);
     message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                       vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
+    ATT_RSTAMP(stp, 187);
 }
 
 template <int PTT, bool F32>

@@ -183,6 +183,11 @@ hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, in
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
                            int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
                            Ragged rg = {});
+// H3 split partials (nsplit) -> one combined split (opart1 [B][Npad][CH] in the
+// h3 tiling, ml1 = (0, 1)) that pw_mid / pw_last read with nsplit = 1 (small
+// batches: combine16's per-thread load chain is the pointwise launch's latency).
+hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int Npad, int nsplit, float *opart1,
+                               float *ml1, hipStream_t s);
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
                          float *vexp, hipStream_t s);

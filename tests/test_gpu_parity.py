@@ -261,8 +261,8 @@ def _fusion_outputs(dev, B=64, N=1000):
                                                   seeds=seeds).items()}
 
 
-def _dump_fusion_outputs(path):  # child process entry (PDSC_FUSE=0)
-    np.savez(path, **_fusion_outputs(torch.device("cuda:0")))
+def _dump_fusion_outputs(path, B=64, N=1000):  # child process entry (A/B knobs set by the parent)
+    np.savez(path, **_fusion_outputs(torch.device("cuda:0"), B, N))
 
 
 def test_fused_encoder_bit_identical(gpu_device, tmp_path):
@@ -288,6 +288,28 @@ def test_fused_encoder_bit_identical(gpu_device, tmp_path):
     ref = np.load(out)
     for k, v in ours.items():
         assert np.array_equal(v, ref[k]), k
+
+
+def test_precombine_bit_identical(gpu_device, tmp_path):
+    """Small batches combine the split-K attention partials in their own launch
+    (combine_rows_kernel, one split handed to pw_mid / pw_last) instead of in
+    the pointwise kernel's prologue: the same bits as the in-kernel combine (a
+    child process with PDSC_PRECOMBINE=0), encoder and forward: a single pair
+    (16 key splits) and a ragged-tail N."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for B, N in ((1, 1000), (1, 1500)):
+        ours = _fusion_outputs(gpu_device, B, N)
+        out = tmp_path / f"inkernel_{B}_{N}.npz"
+        env = dict(os.environ, PDSC_PRECOMBINE="0")
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = np.load(out)
+        for k, v in ours.items():
+            assert np.array_equal(v, ref[k]), (B, N, k)
 
 
 def test_graph_replay_equals_eager(gpu_device):
