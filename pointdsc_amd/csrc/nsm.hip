@@ -32,10 +32,20 @@ namespace pdsc {
 // acc_row(r, h)): each store instruction writes 128 contiguous bytes.
 constexpr int KNN_KPB = 5;
 
+// order-preserving float -> uint key (+0 and -0 share a key, like float ==).
+// The kNN distance rows are stored as these keys (knn_select ranks keys; the
+// distances themselves are never read back).
+PDSC_DEV uint32_t fkey(float f) {
+    if (f == 0.0f) f = 0.0f;
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
 __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
                                                        const int *__restrict__ seeds, int Nstr, int Sstr,
                                                        float *__restrict__ dist, Ragged rg) {
     __shared__ f16x8 Bt[32 * 32];
+    uint32_t *dkey = reinterpret_cast<uint32_t *>(dist);
     const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, l32 = lane & 31;
     // this pair's keys and seeds; Nstr, Sstr: the batch's strides (rows [b][s] of
@@ -85,7 +95,7 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int s = s0 + acc_row(r, h);
-                if (s < S) dist[((size_t)b * Sstr + s) * Nstr + j] = 2.0f - 2.0f * acc[r];
+                if (s < S) dkey[((size_t)b * Sstr + s) * Nstr + j] = fkey(2.0f - 2.0f * acc[r]);
             }
         }
     }
@@ -107,6 +117,7 @@ hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, i
 __global__ __launch_bounds__(256) void knn_dist_f32_kernel(const float *__restrict__ normed,
                                                            const int *__restrict__ seeds, int Nstr, int Sstr,
                                                            float *__restrict__ dist, Ragged rg) {
+    uint32_t *dkey = reinterpret_cast<uint32_t *>(dist);
     const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int h = lane >> 5, l32 = lane & 31;
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);  // this pair's keys and seeds
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(256) void knn_dist_f32_kernel(const float *__restri
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int sr = s0 + acc_row(r, h);
-                if (sr < S) dist[((size_t)b * Sstr + sr) * Nstr + j] = 2.0f - 2.0f * acc[r];
+                if (sr < S) dkey[((size_t)b * Sstr + sr) * Nstr + j] = fkey(2.0f - 2.0f * acc[r]);
             }
         }
     }
@@ -165,13 +176,6 @@ hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStre
     const size_t n = rows * CH;
     hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, rows, out);
     return hipGetLastError();
-}
-
-// order-preserving float -> uint key (+0 and -0 share a key, like float ==)
-PDSC_DEV uint32_t fkey(float f) {
-    if (f == 0.0f) f = 0.0f;
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
 // topk(k+1, smallest) of one seed row, one WAVE per seed (4 per workgroup).
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     // this pair's keys and seeds; Nstr, Sstr: the batch's strides
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
     if (s >= S) return;  // wave-uniform; no workgroup barriers below
-    const float *row = dist + ((size_t)b * Sstr + s) * Nstr;
+    const uint32_t *row = reinterpret_cast<const uint32_t *>(dist) + ((size_t)b * Sstr + s) * Nstr;  // fkey keys
     const uint32_t want = k + 1;
     // Fast path (no atomics): tau0 = the want-th smallest of the 64 per-lane
     // minima bounds the want-th smallest key from above (at least `want` keys are
@@ -227,12 +231,12 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             for (int i4 = 0; i4 < R / 4; ++i4) {
                 const int j = 256 * i4 + 4 * lane;
                 if (vec && j + 3 < N) {
-                    const f32x4 v = *reinterpret_cast<const f32x4 *>(row + j);
+                    const u32x4 v = *reinterpret_cast<const u32x4 *>(row + j);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = fkey(v[e]);
+                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = v[e];
                 } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = j + e < N ? fkey(row[j + e]) : 0xffffffffu;
+                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = j + e < N ? row[j + e] : 0xffffffffu;
                 }
             }
         }
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 return key[i];
             } else {
                 const int j = lane + 64 * i;
-                return j < N ? fkey(row[j]) : 0xffffffffu;
+                return j < N ? row[j] : 0xffffffffu;
             }
         };
         uint32_t lmin = 0xffffffffu;
@@ -282,10 +286,18 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             const int i0 = e0 < (int)c ? fidxb[wave][e0] : 0x7fffffff;
             const uint32_t k1 = e1 < (int)c ? fkeyb[wave][e1] : 0xffffffffu;
             const int i1 = e1 < (int)c ? fidxb[wave][e1] : 0x7fffffff;
+            // ranks by (key, index): candidate m broadcast from lane m % 64 by
+            // v_readlane (no LDS round trip per candidate)
             uint32_t r0 = 0, r1 = 0;
-            for (int m = 0; m < (int)c; ++m) {
-                const uint32_t mu = fkeyb[wave][m];
-                const int mi = fidxb[wave][m];
+            for (int m = 0; m < min((int)c, 64); ++m) {
+                const uint32_t mu = __builtin_amdgcn_readlane(k0, m);
+                const int mi = __builtin_amdgcn_readlane(i0, m);
+                r0 += (mu < k0) || (mu == k0 && mi < i0);
+                r1 += (mu < k1) || (mu == k1 && mi < i1);
+            }
+            for (int m = 64; m < (int)c; ++m) {
+                const uint32_t mu = __builtin_amdgcn_readlane(k1, m - 64);
+                const int mi = __builtin_amdgcn_readlane(i1, m - 64);
                 r0 += (mu < k0) || (mu == k0 && mi < i0);
                 r1 += (mu < k1) || (mu == k1 && mi < i1);
             }
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     const int NI = (N + 63) / 64;
     auto K = [&](int i) -> uint32_t {
         const int j = lane + 64 * i;
-        return j < N ? fkey(row[j]) : 0xffffffffu;
+        return j < N ? row[j] : 0xffffffffu;
     };
     uint32_t kmin = 0xffffffffu, kmax = 0u;
     for (int i = 0; i < NI; ++i) {
@@ -474,11 +486,18 @@ constexpr int KMAX = 64;
 // at a time.  hist[t][a] = iterate t+1; returns bit t = allclose(v_{t+1}, v_t).
 // KC: k rounded up to a multiple of 16 (columns past k are zero, their FMAs
 // exact no-ops), so k = 40 runs 48-long rows instead of KMAX = 64.
+// T's rows in LDS: stride tstride (a multiple of 4), columns k .. KC-1 zero, so
+// every row is KC / 4 unconditional 16-B reads (rows past k read as zero rows).
 template <int KC>
 PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T, float *vbuf, float *hb, int a) {
     float trow[KC];
+    const float *tr = trow_lds + min(a, k - 1) * tstride;
 #pragma unroll
-    for (int c = 0; c < KC; ++c) trow[c] = (a < k && c < k) ? trow_lds[a * tstride + c] : 0.0f;
+    for (int c = 0; c < KC; c += 4) {
+        const f32x4 t4 = *reinterpret_cast<const f32x4 *>(tr + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) trow[c + e] = a < k ? t4[e] : 0.0f;
+    }
     vbuf[a] = 1.0f;
     float v = (a < k) ? 1.0f : 0.0f;
     unsigned flags = 0;
@@ -517,6 +536,24 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
 // same wave runs the power iteration.  No workgroup barriers: waves are
 // independent.
 constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
+// LDS row stride of T for KC-padded rows: 16-B aligned, 13 (KC + 4) / 4 mod 16
+// distinct 16-B banks groups over 16 consecutive rows (conflict-free ds_read_b128)
+__host__ __device__ constexpr int nsm_tstride(int kc) { return kc + 4; }
+// The unordered pairs a < c < KMAX in c-major order (pair p = c (c - 1) / 2 + a,
+// packed a | c << 8): the first k (k - 1) / 2 entries are exactly the pairs of
+// a k-neighbourhood, for every k -- one table load per pair instead of a
+// square-root index decode.
+struct NsmPairs {
+    unsigned short v[KMAX * (KMAX - 1) / 2];
+};
+constexpr NsmPairs make_nsm_pairs() {
+    NsmPairs t{};
+    int p = 0;
+    for (int c = 1; c < KMAX; ++c)
+        for (int a = 0; a < c; ++a) t.v[p++] = (unsigned short)(a | (c << 8));
+    return t;
+}
+static __constant__ const NsmPairs g_nsm_pairs = make_nsm_pairs();
 
 // F32 (PDSC_PRECISION_F32): the Gram tiles on exact fp32 MFMA from the fp32
 // normed rows (`feats` = normed [B][N][128]); H3: `feats` = the split copy.
@@ -533,16 +570,16 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.y, s = blockIdx.x * (blockDim.x >> 6) + wave;
     if (s >= rg.s(b, S)) return;  // wave-uniform (a ragged pair's own seed count; S, N: the strides)
-    const int tls = k + 1;
-    float *Tl = nsm_sdyn + (size_t)wave * (k * tls + KMAX * NSM_PSTR + KMAX);
-    float *P = Tl + k * tls;  // [KMAX][NSM_PSTR]: src xyz, tgt xyz
-    float *vb = P + KMAX * NSM_PSTR;
+    const int tls = nsm_tstride(KC);
+    float *Tl = nsm_sdyn + (size_t)wave * (k * tls + k * NSM_PSTR + 64);
+    float *P = Tl + k * tls;  // [k][NSM_PSTR]: src xyz, tgt xyz
+    float *vb = P + k * NSM_PSTR;
     const float sig = sigma_p[0], sd = sigma_d_p[0];
     const float sig2 = sig * sig, sd2 = sd * sd;
     const float rsig2 = 1.0f / sig2, rsd2 = 1.0f / sd2;
     const int *kr = knn + ((size_t)b * S + s) * k;
     const int idx = min(max(kr[lane < k ? lane : 0], 0), N - 1);
-    {
+    if (lane < k) {
         const float *ps = src + ((size_t)b * N + idx) * 3, *pt = tgt + ((size_t)b * N + idx) * 3;
         *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{ps[0], ps[1], ps[2], pt[0]};
         *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{pt[1], pt[2], 0.0f, 0.0f};
@@ -611,15 +648,15 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         gstore(G11, 1, 1);
     }
     if (lane < k) Tl[lane * tls + lane] = 0.0f;  // diag 0 (:278)
+    for (int a0 = 0; a0 < k; a0 += 4) {  // pad columns k .. KC-1 (KC - k < 16): 4 rows x 16 columns per pass
+        const int a = a0 + (lane >> 4), c = k + (lane & 15);
+        if (a < k && c < KC) Tl[a * tls + c] = 0.0f;
+    }
     __builtin_amdgcn_wave_barrier();  // P and the Gram triangle visible to the wave
-    const int npair = k * (k - 1) / 2, k2 = 2 * k - 1;
+    const int npair = k * (k - 1) / 2;
     for (int p = lane; p < npair; p += 64) {
-        // row a: pairs before it S(a) = a (2k - 1 - a) / 2 <= p < S(a + 1)
-        int a = (int)(0.5f * ((float)k2 - sqrtf((float)(k2 * k2 - 8 * p))));
-        a = max(0, min(a, k - 2));
-        if ((a + 1) * (k2 - a - 1) / 2 <= p) ++a;
-        if (a * (k2 - a) / 2 > p) --a;
-        const int c = p - a * (k2 - a) / 2 + a + 1;
+        const unsigned pc = g_nsm_pairs.v[p];
+        const int a = (int)(pc & 255u), c = (int)(pc >> 8);
         const float g = Tl[a * tls + c];
         const f32x4 pa0 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR);
         const f32x4 pa1 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR + 4);
@@ -648,7 +685,8 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
 }
 
 size_t nsm_seed_lds_bytes(int k, int wpb) {
-    return (size_t)wpb * (k * (k + 1) + KMAX * NSM_PSTR + KMAX) * sizeof(float);
+    const int kc = (k + 15) / 16 * 16;
+    return (size_t)wpb * (k * nsm_tstride(kc) + k * NSM_PSTR + 64) * sizeof(float);
 }
 
 hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const float *tgt, const int *knn, int B,
