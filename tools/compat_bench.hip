@@ -36,7 +36,11 @@ __global__ __launch_bounds__(256) void store_packed(int N, int ntile, float *M) 
     for (int rr = 0; rr < 4; ++rr) {
         const int r = rq + 16 * rr, tr = 2 * ti + (r >> 5);
         if (tr > tc || tr >= nt32 || tc >= nt32) continue;
+#ifdef COMPAT_NT
+        __builtin_nontemporal_store(f32x4{1, 2, 3, 4}, reinterpret_cast<f32x4 *>(M + (size_t)mpack_tile(tr, tc, nt32) * 1024 + (r & 31) * 32 + ((cq * 4) & 31)));
+#else
         *reinterpret_cast<f32x4 *>(M + (size_t)mpack_tile(tr, tc, nt32) * 1024 + (r & 31) * 32 + ((cq * 4) & 31)) = f32x4{1, 2, 3, 4};
+#endif
     }
 }
 // store-only, whole rows: block = 4 rows, thread = 16 B columns strided
