@@ -76,6 +76,12 @@ def assert_seeds_equivalent(ours, ref, scores, tol=0.0):
 ENVELOPE = 2.5
 FEAT_FLOOR = 1e-6   # x max|f|
 LOGIT_FLOOR = 2e-6
+# ... and in bulk: the HIP path's RMS distance from exact arithmetic is at most BULK
+# times the largest RMS distance of the fp32 realisations (measured r03: <= 1.00x
+# on every golden in both precision modes), so a regression that scales every
+# error up fails here even where one amplified point sets a loose max-error bar.
+BULK = 1.5
+RMS_FLOOR = 1e-8
 
 
 def encoder_torch(g, sd, dev, dtype=None, seed=None):
@@ -129,22 +135,31 @@ def encoder_fp64(g, sd, dev):
 FP32_REALISATIONS = 4
 
 
-def fp32_envelope(g, sd, dev):
+def rms(x):
+    return float(np.sqrt(np.mean(np.square(x))))
+
+
+def fp32_envelope(g, sd, dev, bulk=False):
     """The fp32 noise of this network on this input: the largest distance from exact
     arithmetic (fp64) of the reference's own outputs and of FP32_REALISATIONS
     re-ordered torch-fp32 evaluations.  Returns (feature error / max|f|, logit
-    error, f64, c64, max|f|).  The reference's features are not stored for
-    N > 5000; the realisations still measure that case's fp32 noise."""
+    error, f64, c64, max|f|), and with `bulk` also the bulk noise: the largest RMS
+    distance of the realisations (features / max|f|, logits).  The reference's
+    features are not stored for N > 5000; the realisations still measure that
+    case's fp32 noise."""
     import torch
     f64, c64 = encoder_fp64(g, sd, dev)
     mx = np.abs(f64).max()
     e_f = np.abs(g["corr_features"] - f64).max() / mx if len(g["corr_features"]) else 0.0
     e_c = np.abs(g["confidence"] - c64).max()
+    r_f = r_c = 0.0
     for s in range(FP32_REALISATIONS):
         f32, c32 = encoder_torch(g, sd, dev, torch.float32, seed=s)
         e_f = max(e_f, np.abs(f32 - f64).max() / mx)
         e_c = max(e_c, np.abs(c32 - c64).max())
-    return e_f, e_c, f64, c64, mx
+        r_f = max(r_f, rms(f32 - f64) / mx)
+        r_c = max(r_c, rms(c32 - c64))
+    return (e_f, e_c, f64, c64, mx, r_f, r_c) if bulk else (e_f, e_c, f64, c64, mx)
 
 
 def assert_seeds_near_ties(seeds, conf, g, tol):

@@ -16,10 +16,11 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import (ENVELOPE, FEAT_FLOOR, LOGIT_FLOOR, assert_knn_equivalent, assert_poses_close, assert_rigid,
+from conftest import (BULK, ENVELOPE, FEAT_FLOOR, LOGIT_FLOOR, RMS_FLOOR, assert_knn_equivalent, assert_poses_close,
+                      assert_rigid,
                       assert_seeds_equivalent,
                       assert_seeds_near_ties, fp32_envelope, golden_hparams, golden_names, golden_state_dict,
-                      load_golden, seed_H_rank)
+                      load_golden, rms, seed_H_rank)
 
 pytestmark = pytest.mark.gpu
 
@@ -47,6 +48,16 @@ def _inputs(g, dev):
     return (_t(g["corr_pos"][None], dev), _t(g["src_keypts"][None], dev), _t(g["tgt_keypts"][None], dev))
 
 
+def _bulk(name, g, dev):
+    """(fp32 bulk feature noise / max|f|, fp32 bulk logit noise): the RMS distances, cached."""
+    key = name + "#bulk"
+    if key not in _FP64:
+        e_f, e_c, f64, c64, mx, r_f, r_c = fp32_envelope(g, golden_state_dict(g), dev, bulk=True)
+        _FP64[name] = (e_f, e_c, f64, c64, mx)
+        _FP64[key] = (r_f, r_c)
+    return _FP64[key]
+
+
 def _envelope(name, g, dev):
     """(fp32 feature noise / max|f|, fp32 logit noise, f64, c64, max|f|): conftest.fp32_envelope, cached."""
     if name not in _FP64:
@@ -72,19 +83,25 @@ def test_compat(name, gpu_device):
 @pytest.mark.parametrize("name", NAMES)
 def test_encoder_and_classifier(name, precision, gpu_device):
     """a2-a4: features, normed features and logits within ENVELOPE x the reference's
-    own distance from exact arithmetic (plus an fp32-resolution floor)."""
+    own distance from exact arithmetic (plus an fp32-resolution floor), and in
+    bulk (RMS) within BULK x the fp32 realisations'."""
     from pointdsc_amd import kernels
     g = load_golden(name)
     m = _model(g, gpu_device, precision)
     corr, src, tgt = _inputs(g, gpu_device)
     M = kernels.compat(src, tgt, m.sigma_spat)
     feat, normed, conf = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, M)
+    r_f, r_c = _bulk(name, g, gpu_device)
     e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
     ours_c = np.abs(conf[0].double().cpu().numpy() - c64).max()
     assert ours_c <= ENVELOPE * e_c + LOGIT_FLOOR, (ours_c, e_c)
     f = feat[0].double().cpu().numpy()
     ours_f = np.abs(f - f64).max() / mx
     assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (ours_f, e_f)
+    # in bulk too (conftest.BULK): RMS distance from exact arithmetic vs the fp32 realisations'
+    rms_f, rms_c = rms(f - f64) / mx, rms(conf[0].double().cpu().numpy() - c64)
+    assert rms_f <= BULK * r_f + RMS_FLOOR, (rms_f, r_f)
+    assert rms_c <= BULK * r_c + RMS_FLOOR, (rms_c, r_c)
     # normed rows are unit vectors: their error is the feature error relative to the row norm
     n64 = f64 / np.maximum(np.linalg.norm(f64, axis=1, keepdims=True), 1e-12)
     rel_row = (np.abs(f - f64).max(1) / np.maximum(np.linalg.norm(f64, axis=1), 1e-12)).max()

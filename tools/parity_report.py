@@ -42,7 +42,7 @@ def report(name, precision, dev):
     cfg, packed = m.pdsc_config(), m.packed_weights()
     M = kernels.compat(src, tgt, m.sigma_spat)
     feat, normed, conf = kernels.encoder(cfg, packed, corr, M)
-    e_f, e_c, f64, c64, _ = fp32_envelope(g, golden_state_dict(g), dev)
+    e_f, e_c, f64, c64, _, r_f, r_c = fp32_envelope(g, golden_state_dict(g), dev, bulk=True)
     has_f = len(g["corr_features"]) > 0
     f_ref = g["corr_features"].astype(np.float64) if has_f else f64
     f = feat[0].double().cpu().numpy()
@@ -58,6 +58,10 @@ def report(name, precision, dev):
     out["ref_vs_fp64_logit"] = float(np.abs(g["confidence"] - c64).max())
     out["ours_vs_fp64_logit"] = float(np.abs(conf[0].double().cpu().numpy() - c64).max())
     out["fp32_noise_feat"], out["fp32_noise_logit"] = float(e_f), float(e_c)
+    # bulk (RMS) error against the largest RMS of the fp32 realisations
+    from conftest import rms
+    out["rms_ratio_feat"] = float(rms(f - f64) / mx / r_f) if r_f > 0 else None
+    out["rms_ratio_logit"] = float(rms(conf[0].double().cpu().numpy() - c64) / r_c) if r_c > 0 else None
     from oracle import pdsc_oracle as O
     lm_o = O.local_max(g["src_keypts"], conf[0].cpu().numpy(), float(g["nms_radius"]))
     out["lm_mismatch"] = int((lm_o != g["is_local_max"]).sum())
