@@ -260,8 +260,33 @@ struct AttnGridH3 {
     PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
+// Key splits per query block: the count that minimises the estimated launch
+// time  ceil(workgroups / slots) x (key tiles per split + H3_SPLIT_C0)  --
+// whole rounds of `slots` resident workgroups (2 per CU), each as long as its
+// workgroups' tile loop plus a fixed per-workgroup cost (prologue, first DMA,
+// partial stores, the combine's extra reads) of about H3_SPLIT_C0 tiles.
+// Measured (A/B, one box): N = 5000 x 8 pairs 313 us per layer at 4 splits
+// (2.5 rounds) against 350 at 2 (1.25 rounds: a quarter-full last round) and
+// 324-326 at 5 / 8; 16 x 1000 best at 4 (one round).  Ties: fewer splits.
+constexpr int H3_SPLIT_C0 = 15;
+inline int attention_split_count(long blocks, int nst, int slots) {
+    int best = 1;
+    long best_cost = -1;
+    for (int ns = 1; ns <= std::max(1, nst / 2); ++ns) {
+        const int sps = (nst + ns - 1) / ns;
+        if ((nst + sps - 1) / sps != ns) continue;  // an equivalent smaller count exists
+        const long rounds = (blocks * ns + slots - 1) / slots;
+        const long cost = rounds * (sps + H3_SPLIT_C0);
+        if (best_cost < 0 || cost < best_cost) {
+            best = ns;
+            best_cost = cost;
+        }
+    }
+    return best;
+}
+
 template <int NW>
-inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
+inline AttnGridH3 attention_h3_grid(int B, int N, int slots) {
     AttnGridH3 g;
     g.nv = nullptr;
     g.B = B;
@@ -269,8 +294,7 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int target) {
     g.Npad = round_up(N, QB);
     g.nqb = (N + NW * 32 - 1) / (NW * 32);
     const int nst = (N + H3_TILE - 1) / H3_TILE;
-    int ns = (target + B * g.nqb - 1) / (B * g.nqb);
-    ns = std::max(1, std::min(ns, std::max(1, nst / 2)));
+    const int ns = attention_split_count((long)B * g.nqb, nst, slots);
     g.sps = (nst + ns - 1) / ns;
     g.nsplit = (nst + g.sps - 1) / g.sps;
     return g;

@@ -128,9 +128,10 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s) {
 // the exact-fp32-MFMA kernel of attention.hpp.)
 constexpr int ATT_NW = 4;
 
-// Target workgroup count of the split-K decomposition (A/B knob, measurement
-// only: PDSC_ATT_TARGET overrides the default 512 for the whole process; 512
-// measured 6 % faster per step than 1024 at 64 pairs x N = 1000).
+// Resident workgroups per round of the split-K decomposition (2 per CU on 256
+// CUs; attention_split_count).  A/B knob, measurement only: PDSC_ATT_TARGET
+// overrides it for the whole process.  (The exact-fp32 attention keeps its
+// round-2 rule: splits = ceil(target / blocks).)
 static int att_target() {
     static const int t = [] {
         const char *e = getenv("PDSC_ATT_TARGET");
