@@ -1491,15 +1491,18 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_last_kernel(
 }
 #undef PW2_PROLOGUE
 
-// pw2 for launches of at least two 128-point workgroups per CU (knob PDSC_PW2:
-// 0 never, 2 always, else this rule; measurement only).
+// pw2 for launches of at least 320 128-point workgroups, 1.25 per CU (knob
+// PDSC_PW2: 0 never, 2 always, else this rule; measurement only).  Measured
+// encoder ms, pw2 vs pw_mid chains: 8 x N=5000 (320 WGs; 3 key splits) 4.48
+// vs 4.61; 40 x 1000 (320, fused) 1.47 vs 1.78; 56 x 1000 (448, fused) 1.68 vs
+// 2.12; 32 x 1000 (256) 1.26 vs 1.22 and 1.24 fused; 16 x 1000 (128) 0.95 vs 0.80.
 static bool use_pw2(int B, int Npad, bool f32) {
     static const int mode = [] {
         const char *e = getenv("PDSC_PW2");
         return e ? atoi(e) : 1;
     }();
     if (f32 || mode == 0) return false;
-    return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) * PW2_W >= 2048;  // >= 2 waves per SIMD
+    return mode == 2 || (long)B * ((Npad + PW2_PTS - 1) / PW2_PTS) >= 320;
 }
 
 static W2Sched sched_qkv(W2Sched S, const PwDense4 &d) {

@@ -41,7 +41,7 @@ PDSC_DEV uint32_t fkey(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restrict__ ns,
+__global__ __launch_bounds__(256, 4) void knn_dist_kernel(const _Float16 *__restrict__ ns,
                                                        const int *__restrict__ seeds, int Nstr, int Sstr,
                                                        float *__restrict__ dist, Ragged rg) {
     __shared__ f16x8 Bt[32 * 32];
@@ -68,14 +68,23 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
     }
     const int nkt = (N + 31) / 32;
     const int t0 = blockIdx.x * KNN_KPB, t1 = min(t0 + KNN_KPB, nkt);
-    for (int t = t0; t < t1; ++t) {
-        const int j0 = t * 32;
-        f16x8 stage[4];
+    // the wave's 32 seed rows through a buffer resource: rows past S fall outside
+    // it (their stores are dropped), row r's offset is an SGPR operand
+    const uint32_t rowb = (uint32_t)Nstr * 4u;
+    const __amdgpu_buffer_rsrc_t rd =
+        h3_rsrc(dkey + ((size_t)b * Sstr + min(s0, S)) * Nstr, (uint32_t)max(min(32, S - s0), 0) * rowb);
+    // key tile t+1 is loaded into registers while tile t computes and stores
+    f16x8 stage[4];
+    auto load_tile = [&](int t) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = tid + 256 * q, r = e >> 5, c = e & 31;
-            stage[q] = reinterpret_cast<const f16x8 *>(F + (size_t)min(j0 + r, N - 1) * 2 * CH)[c];
+            stage[q] = reinterpret_cast<const f16x8 *>(F + (size_t)min(t * 32 + r, N - 1) * 2 * CH)[c];
         }
+    };
+    if (t0 < t1) load_tile(t0);
+    for (int t = t0; t < t1; ++t) {
+        const int j0 = t * 32;
         __syncthreads();  // the previous tile's readers are done
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -83,6 +92,7 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
             Bt[r * 32 + (c & 16) + ((c & 15) ^ (r & 15))] = stage[q];
         }
         __syncthreads();
+        if (t + 1 < t1) load_tile(t + 1);
         if (!active) continue;
         const int j = j0 + l32;
         f32x16 acc = zero16();
@@ -92,11 +102,11 @@ __global__ __launch_bounds__(256) void knn_dist_kernel(const _Float16 *__restric
             acc = mfma_h3(ah[i], al[i], Bt[l32 * 32 + cc], Bt[l32 * 32 + 16 + cc], acc);
         }
         if (j < N) {
+            const uint32_t vo = 4u * j + (uint32_t)(4 * h) * rowb;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int s = s0 + acc_row(r, h);
-                if (s < S) dkey[((size_t)b * Sstr + s) * Nstr + j] = fkey(2.0f - 2.0f * acc[r]);
-            }
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b32(fkey(2.0f - 2.0f * acc[r]), rd, vo,
+                                                      (uint32_t)((r & 3) + 8 * (r >> 2)) * rowb, 0);
         }
     }
 }
@@ -226,17 +236,24 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         // index of this lane's i-th key
         auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
         if constexpr (R > 0) {
-            const bool vec = (Nstr & 3) == 0;  // rows 16-B aligned
+            // buffer loads over the row (lane offset in one VGPR, the key
+            // block's offset in the SGPR operand; past the row they return 0),
+            // branch-free, so all R/4 (or R) loads are in flight together and no
+            // per-load 64-bit addresses stay live; keys past N are selected away
+            const __amdgpu_buffer_rsrc_t rr = h3_rsrc(row, (uint32_t)Nstr * 4u);
+            if ((Nstr & 3) == 0) {  // rows 16-B aligned (wave-uniform)
 #pragma unroll
-            for (int i4 = 0; i4 < R / 4; ++i4) {
-                const int j = 256 * i4 + 4 * lane;
-                if (vec && j + 3 < N) {
-                    const u32x4 v = *reinterpret_cast<const u32x4 *>(row + j);
+                for (int i4 = 0; i4 < R / 4; ++i4) {
+                    const u32x4 v = __builtin_bit_cast(
+                        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, 16u * lane, 1024u * i4, 0));
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = v[e];
-                } else {
+                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = 256 * i4 + 4 * lane + e < N ? v[e] : 0xffffffffu;
+                }
+            } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) key[4 * i4 + e] = j + e < N ? row[j + e] : 0xffffffffu;
+                for (int i = 0; i < R; ++i) {
+                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rr, 16u * lane, 4u * (256 * (i >> 2) + (i & 3)), 0);
+                    key[i] = 256 * (i >> 2) + 4 * lane + (i & 3) < N ? v : 0xffffffffu;
                 }
             }
         }
@@ -251,7 +268,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         uint32_t lmin = 0xffffffffu;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
-            if (J(i) < N) lmin = min(lmin, K(i));
+            if (R > 0 || J(i) < N) lmin = min(lmin, K(i));  // R > 0: keys past N are ~0u
         // tau0 = the want-th smallest lane minimum: the smallest value v with
         // #{lanes: lmin <= v} >= want, built bit by bit from the top (one
         // compare + ballot + scalar popcount per bit instead of 64 readlanes)
@@ -261,10 +278,14 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             if ((uint32_t)__popcll(__ballot(lmin <= probe)) < want) tau0 |= 1u << bit;
         }
         const unsigned long long below = (1ull << lane) - 1ull;
+        // the key indices recomputed from an opaque base: otherwise the compiler
+        // keeps the R load-time indices live across the threshold search
+        int lb = R > 0 ? 4 * lane : lane;
+        asm volatile("" : "+v"(lb));
         uint32_t c = 0;
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-            const int j = J(i);
+            const int j = R > 0 ? 256 * (i >> 2) + lb + (i & 3) : lb + 64 * i;
             const uint32_t u = K(i);
             const bool q = j < N && u <= tau0;
             const unsigned long long m = __ballot(q);
@@ -609,23 +630,41 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
             }
         }
     } else {
-        const _Float16 *F = static_cast<const _Float16 *>(feats) + (size_t)b * N * 2 * CH;
-        const _Float16 *r0 = F + (size_t)__shfl(idx, l32) * 2 * CH + 8 * h;
-        const _Float16 *r1 = F + (size_t)__shfl(idx, 32 + l32) * 2 * CH + 8 * h;
-        // rows past k are never read back (the T triangle takes a < c < k):
-        // zero fragments instead of gathering them (k = 40: 40 of 64 rows)
-        const bool v0 = l32 < k, v1 = 32 + l32 < k;
-        const f16x8 z8 = {};
+        // rows past k are never read back (the T triangle takes a < c < k): their
+        // lanes point outside the buffer resource, so those loads return zero
+        // without a gather (k = 40: 40 of 64 rows).  Branch-free buffer loads:
+        // every k-step's fragments can be in flight together (exec-masked loads
+        // in branches were issued one k-step at a time, 16 serial gathers).
+        const __amdgpu_buffer_rsrc_t rF =
+            h3_rsrc(static_cast<const _Float16 *>(feats) + (size_t)b * N * 2 * CH, (uint32_t)N * 4u * CH);
+        const uint32_t oob = 0x80000000u;
+        const uint32_t o0 = l32 < k ? (uint32_t)__shfl(idx, l32) * 4u * CH + 16u * h : oob;
+        const uint32_t o1 = 32 + l32 < k ? (uint32_t)__shfl(idx, 32 + l32) * 4u * CH + 16u * h : oob;
+        auto ld = [&](uint32_t o, int off) {
+            return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rF, o, (uint32_t)off, 0));
+        };
+        // k-step j's four fragments are issued NSM_GLA steps ahead of its MFMAs
+        // (the empty asm keeps the scheduler from sinking them to their uses)
+        constexpr int NSM_GLA = 3;
+        f16x8 fr[8][4];
+        auto issue = [&](int j) {
+            fr[j][0] = ld(o0, 32 * j);
+            fr[j][1] = ld(o0, 2 * CH + 32 * j);
+            if (nt > 1) {
+                fr[j][2] = ld(o1, 32 * j);
+                fr[j][3] = ld(o1, 2 * CH + 32 * j);
+            }
+        };
+#pragma unroll
+        for (int j = 0; j < NSM_GLA; ++j) issue(j);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const f16x8 ah = v0 ? *reinterpret_cast<const f16x8 *>(r0 + 16 * j) : z8;
-            const f16x8 al = v0 ? *reinterpret_cast<const f16x8 *>(r0 + CH + 16 * j) : z8;
-            G00 = mfma_h3(ah, al, ah, al, G00);
+            if (j + NSM_GLA < 8) issue(j + NSM_GLA);
+            asm volatile("" ::: "memory");
+            G00 = mfma_h3(fr[j][0], fr[j][1], fr[j][0], fr[j][1], G00);
             if (nt > 1) {
-                const f16x8 bh = v1 ? *reinterpret_cast<const f16x8 *>(r1 + 16 * j) : z8;
-                const f16x8 bl = v1 ? *reinterpret_cast<const f16x8 *>(r1 + CH + 16 * j) : z8;
-                G01 = mfma_h3(ah, al, bh, bl, G01);
-                G11 = mfma_h3(bh, bl, bh, bl, G11);
+                G01 = mfma_h3(fr[j][0], fr[j][1], fr[j][2], fr[j][3], G01);
+                G11 = mfma_h3(fr[j][2], fr[j][3], fr[j][2], fr[j][3], G11);
             }
         }
     }

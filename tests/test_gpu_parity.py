@@ -286,25 +286,27 @@ def test_fused_encoder_bit_identical(gpu_device, tmp_path):
     """attn_pw2_kernel (attention_l + the pointwise chain_l in one launch, partials
     kept in registers) gives exactly the bits of the separate attention_h3 +
     pw2_mid launches (run in a child process with the PDSC_FUSE=0 knob): encoder
-    features / confidences with dense M, and the whole forward with packed M."""
+    features / confidences with dense M, and the whole forward with packed M; a
+    two-round headline-like batch and a 1.25-round one (320 workgroups)."""
     import ctypes
     import os
     import subprocess
     import sys
     from pointdsc_amd import _lib
-    fused = ctypes.c_int32()
-    _lib.check(_lib.load().pdsc_encoder_plan(64, 1000, 0, ctypes.byref(fused)), "encoder_plan")
-    assert fused.value == 1
-    ours = _fusion_outputs(gpu_device)
-    out = tmp_path / "unfused.npz"
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, PDSC_FUSE="0")
-    code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
-           f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r})"
-    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
-    ref = np.load(out)
-    for k, v in ours.items():
-        assert np.array_equal(v, ref[k]), k
+    for B, N in ((64, 1000), (40, 1000)):
+        fused = ctypes.c_int32()
+        _lib.check(_lib.load().pdsc_encoder_plan(B, N, 0, ctypes.byref(fused)), "encoder_plan")
+        assert fused.value == 1, (B, N)
+        ours = _fusion_outputs(gpu_device, B, N)
+        out = tmp_path / f"unfused_{B}_{N}.npz"
+        env = dict(os.environ, PDSC_FUSE="0")
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = np.load(out)
+        for k, v in ours.items():
+            assert np.array_equal(v, ref[k]), (B, N, k)
 
 
 def test_precombine_bit_identical(gpu_device, tmp_path):
