@@ -236,12 +236,13 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         // index of this lane's i-th key
         auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
         if constexpr (R > 0) {
-            // buffer loads over the row (lane offset in one VGPR, the key
-            // block's offset in the SGPR operand; past the row they return 0),
-            // branch-free, so all R/4 (or R) loads are in flight together and no
-            // per-load 64-bit addresses stay live; keys past N are selected away
-            const __amdgpu_buffer_rsrc_t rr = h3_rsrc(row, (uint32_t)Nstr * 4u);
             if ((Nstr & 3) == 0) {  // rows 16-B aligned (wave-uniform)
+                // buffer loads over the row's first round_up(N, 4) keys (lane offset
+                // in one VGPR, the key block's offset in the SGPR operand; blocks
+                // past them return 0 without a fetch), branch-free, so all R/4
+                // loads are in flight together and no per-load 64-bit addresses
+                // stay live (97 vs 178 VGPRs at R = 80); keys past N selected away
+                const __amdgpu_buffer_rsrc_t rr = h3_rsrc(row, (uint32_t)((N + 3) & ~3) * 4u);
 #pragma unroll
                 for (int i4 = 0; i4 < R / 4; ++i4) {
                     const u32x4 v = __builtin_bit_cast(
@@ -250,10 +251,12 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                     for (int e = 0; e < 4; ++e) key[4 * i4 + e] = 256 * i4 + 4 * lane + e < N ? v[e] : 0xffffffffu;
                 }
             } else {
+                // exec-masked dword loads (measured faster here than branch-free
+                // buffer or clamped loads: 134 vs 150 / 145 us at 128 x 1289)
 #pragma unroll
                 for (int i = 0; i < R; ++i) {
-                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rr, 16u * lane, 4u * (256 * (i >> 2) + (i & 3)), 0);
-                    key[i] = 256 * (i >> 2) + 4 * lane + (i & 3) < N ? v : 0xffffffffu;
+                    const int j = 256 * (i >> 2) + 4 * lane + (i & 3);
+                    key[i] = j < N ? row[j] : 0xffffffffu;
                 }
             }
         }
@@ -576,6 +579,20 @@ constexpr NsmPairs make_nsm_pairs() {
 }
 static __constant__ const NsmPairs g_nsm_pairs = make_nsm_pairs();
 
+#ifdef ATT_STAMPS
+// Diagnostic build: stamps of 64 evenly spaced workgroups' waves (tools/nsm_stamps.py).
+PDSC_DEV unsigned long long *nsm_stamp_ptr(int wave) {
+    const int wg = blockIdx.y * gridDim.x + blockIdx.x, str = max(1, (int)(gridDim.x * gridDim.y) / ST_WGS);
+    return (wg % str == 0 && wg / str < ST_WGS && wave < 4) ? g_att_stamps + ((wg / str) * 4 + wave) * ST_PER_WAVE
+                                                            : nullptr;
+}
+#define NSM_STAMP(i) ATT_STAMP(nstp, i)
+#else
+#define NSM_STAMP(i) \
+    do {             \
+    } while (0)
+#endif
+
 // F32 (PDSC_PRECISION_F32): the Gram tiles on exact fp32 MFMA from the fp32
 // normed rows (`feats` = normed [B][N][128]); H3: `feats` = the split copy.
 template <bool F32, int KC>
@@ -591,6 +608,11 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.y, s = blockIdx.x * (blockDim.x >> 6) + wave;
     if (s >= rg.s(b, S)) return;  // wave-uniform (a ragged pair's own seed count; S, N: the strides)
+#ifdef ATT_STAMPS
+    unsigned long long *nstp = nsm_stamp_ptr(wave);
+    ATT_RSTAMP(nstp, 16);
+    NSM_STAMP(0);
+#endif
     const int tls = nsm_tstride(KC);
     float *Tl = nsm_sdyn + (size_t)wave * (k * tls + k * NSM_PSTR + 64);
     float *P = Tl + k * tls;  // [k][NSM_PSTR]: src xyz, tgt xyz
@@ -600,11 +622,19 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     const float rsig2 = 1.0f / sig2, rsd2 = 1.0f / sd2;
     const int *kr = knn + ((size_t)b * S + s) * k;
     const int idx = min(max(kr[lane < k ? lane : 0], 0), N - 1);
-    if (lane < k) {
-        const float *ps = src + ((size_t)b * N + idx) * 3, *pt = tgt + ((size_t)b * N + idx) * 3;
-        *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{ps[0], ps[1], ps[2], pt[0]};
-        *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{pt[1], pt[2], 0.0f, 0.0f};
-    }
+    NSM_STAMP(1);
+    // the neighbour's coordinates: loaded now (every lane's idx is a valid row),
+    // written to LDS once the Gram gathers are in flight, so the two gathers'
+    // latencies overlap
+    const float *ps = src + ((size_t)b * N + idx) * 3, *pt = tgt + ((size_t)b * N + idx) * 3;
+    const float p0 = ps[0], p1 = ps[1], p2 = ps[2], p3 = pt[0], p4 = pt[1], p5 = pt[2];
+    auto store_p = [&] {
+        if (lane < k) {
+            *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{p0, p1, p2, p3};
+            *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{p4, p5, 0.0f, 0.0f};
+        }
+        NSM_STAMP(2);
+    };
     // Gram operands streamed one 16-input k-step at a time (16 VGPRs in
     // flight instead of both whole 32-row fragments): the wave fits in 128
     // VGPRs, 4 waves per SIMD to hide the row gathers.  Accumulation order per
@@ -612,6 +642,7 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     const int nt = (k + 31) / 32;
     f32x16 G00 = zero16(), G01 = zero16(), G11 = zero16();
     if constexpr (F32) {
+        store_p();
         const float *F = static_cast<const float *>(feats) + (size_t)b * N * CH;
         const float *r0 = F + (size_t)__shfl(idx, l32) * CH + 4 * h;
         const float *r1 = F + (size_t)__shfl(idx, 32 + l32) * CH + 4 * h;
@@ -657,6 +688,7 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         };
 #pragma unroll
         for (int j = 0; j < NSM_GLA; ++j) issue(j);
+        store_p();
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             if (j + NSM_GLA < 8) issue(j + NSM_GLA);
@@ -686,6 +718,7 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         gstore(G01, 0, 1);
         gstore(G11, 1, 1);
     }
+    NSM_STAMP(3);
     if (lane < k) Tl[lane * tls + lane] = 0.0f;  // diag 0 (:278)
     for (int a0 = 0; a0 < k; a0 += 4) {  // pad columns k .. KC-1 (KC - k < 16): 4 rows x 16 columns per pass
         const int a = a0 + (lane >> 4), c = k + (lane & 15);
@@ -693,8 +726,12 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     }
     __builtin_amdgcn_wave_barrier();  // P and the Gram triangle visible to the wave
     const int npair = k * (k - 1) / 2;
+    // the pair table entry of the next pass is loaded one pass ahead (a global
+    // load per pass otherwise exposes its whole latency, 13 passes at k = 40)
+    unsigned pc_next = g_nsm_pairs.v[min(lane, npair - 1)];
     for (int p = lane; p < npair; p += 64) {
-        const unsigned pc = g_nsm_pairs.v[p];
+        const unsigned pc = pc_next;
+        pc_next = g_nsm_pairs.v[min(p + 64, npair - 1)];
         const int a = (int)(pc & 255u), c = (int)(pc >> 8);
         const float g = Tl[a * tls + c];
         const f32x4 pa0 = *reinterpret_cast<const f32x4 *>(P + a * NSM_PSTR);
@@ -717,7 +754,12 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         Tl[c * tls + a] = val;
     }
     __builtin_amdgcn_wave_barrier();
+    NSM_STAMP(4);
     const unsigned flags = power_iterate<KC>(Tl, tls, k, T, vb, hist + ((size_t)b * S + s) * T * k, lane);
+    NSM_STAMP(5);
+#ifdef ATT_STAMPS
+    ATT_RSTAMP(nstp, 17);
+#endif
     // this seed's allclose bits; nsm_finish ANDs a pair's seeds (a per-pair
     // atomicAnd here serialised S atomics per address: 30-60 us of the launch)
     if (lane == 0) seed_flags[(size_t)b * S + s] = flags;
@@ -1120,5 +1162,17 @@ hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb,
     hipLaunchKernelGGL(rigid_kernel, dim3(nb), dim3(RB), 0, s, A, Bp, w, n, trans);
     return hipGetLastError();
 }
+
+#ifdef ATT_STAMPS
+extern "C" int pdsc_diag_nsm_stamps(void *host, size_t bytes) {
+    const size_t n = std::min(bytes, sizeof(g_att_stamps));
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int pdsc_diag_nsm_stamps_clear() {
+    static unsigned long long zero[ST_WGS * 4 * ST_PER_WAVE];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_att_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess ? 0
+                                                                                                             : -1;
+}
+#endif
 
 }  // namespace pdsc
