@@ -43,7 +43,7 @@ PDSC_DEV uint32_t fkey(float f) {
 
 __global__ __launch_bounds__(256, 4) void knn_dist_kernel(const _Float16 *__restrict__ ns,
                                                        const int *__restrict__ seeds, int Nstr, int Sstr,
-                                                       float *__restrict__ dist, Ragged rg) {
+                                                       int kpb, float *__restrict__ dist, Ragged rg) {
     __shared__ f16x8 Bt[32 * 32];
     uint32_t *dkey = reinterpret_cast<uint32_t *>(dist);
     const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256, 4) void knn_dist_kernel(const _Float16 *__rest
     // this pair's keys and seeds; Nstr, Sstr: the batch's strides (rows [b][s] of
     // dist are Nstr long)
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
-    if (blockIdx.y * 128 >= S || blockIdx.x * KNN_KPB * 32 >= N) return;  // workgroup-uniform
+    if (blockIdx.y * 128 >= S || blockIdx.x * kpb * 32 >= N) return;  // workgroup-uniform
     const int s0 = (blockIdx.y * 4 + wave) * 32;
     const bool active = s0 < S;  // wave-uniform; every wave joins the barriers
     const _Float16 *F = ns + (size_t)b * Nstr * 2 * CH;
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256, 4) void knn_dist_kernel(const _Float16 *__rest
         }
     }
     const int nkt = (N + 31) / 32;
-    const int t0 = blockIdx.x * KNN_KPB, t1 = min(t0 + KNN_KPB, nkt);
+    const int t0 = blockIdx.x * kpb, t1 = min(t0 + kpb, nkt);
     // the wave's 32 seed rows through a buffer resource: rows past S fall outside
     // it (their stores are dropped), row r's offset is an SGPR operand
     const uint32_t rowb = (uint32_t)Nstr * 4u;
@@ -114,8 +114,12 @@ __global__ __launch_bounds__(256, 4) void knn_dist_kernel(const _Float16 *__rest
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,
                            hipStream_t s, Ragged rg) {
     const int nkt = (N + 31) / 32;
-    hipLaunchKernelGGL(knn_dist_kernel, dim3((nkt + KNN_KPB - 1) / KNN_KPB, (S + 127) / 128, B), dim3(256), 0, s,
-                       ns, seeds, N, S, dist, rg);
+    // key tiles per workgroup: KNN_KPB, or 1 when that leaves fewer than 256
+    // workgroups (a single N = 1000 pair: 32 instead of 7)
+    const long wg5 = (long)((nkt + KNN_KPB - 1) / KNN_KPB) * ((S + 127) / 128) * B;
+    const int kpb = wg5 >= 256 ? KNN_KPB : 1;
+    hipLaunchKernelGGL(knn_dist_kernel, dim3((nkt + kpb - 1) / kpb, (S + 127) / 128, B), dim3(256), 0, s,
+                       ns, seeds, N, S, kpb, dist, rg);
     return hipGetLastError();
 }
 
