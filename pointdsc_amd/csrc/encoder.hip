@@ -476,9 +476,9 @@ enum SplitMode { SPLIT_Q = 0, SPLIT_K = 1, SPLIT_V = 2 };
 // fragment read -- 32 rows, one chunk each -- is conflict-free).  Shared by the
 // Q, K and V products instead of re-splitting per wave and per product.
 constexpr int XS_ROWB = 2 * CH * 2;  // bytes per split row
-template <int PTT>
+template <int PTT, int NT = 256>
 PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
-    constexpr int TPR = 256 / PTT, CPT = 16 / TPR;  // threads per row, chunks per thread
+    constexpr int TPR = NT / PTT, CPT = 16 / TPR;  // threads per row, chunks per thread
     const int r = tid / TPR;
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
@@ -494,14 +494,16 @@ PDSC_DEV void split_tile(const float *X, int xstr, char *Xs, int tid) {
 // SPLIT_V also sets the tile exponents vexp[p0/32 + i] (attention_h3.hpp) from
 // the max |v| over the 4 waves' channel tiles, exchanged through `red` (LDS,
 // 4 * NRT floats no other wave reads at this point; one barrier).
+// active = false (8-wave workgroups, SPLIT_V): the wave only joins the barrier.
 template <int MODE, int NRT>
 PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const float *__restrict__ pk,
                           const DenseOff &off, int ct, _Float16 *__restrict__ dst, int p0, int lane,
-                          float *red = nullptr, float *__restrict__ vexp = nullptr) {
+                          float *red = nullptr, float *__restrict__ vexp = nullptr, bool active = true) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
 #pragma unroll
     for (int i = 0; i < NRT; ++i) acc[i] = zero16();
+    if (active)
 #pragma unroll
     for (int ks = 0; ks < CH / 16; ++ks) {
 #pragma unroll
@@ -519,6 +521,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
         const int c = ct * 32 + l32;
         const float bias = pk[off.bias + c];
         int ev[NRT];
+        if (active)
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
             float m = 0.0f;
@@ -531,6 +534,7 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
             if (lane == 0) red[4 * i + ct] = m;
         }
         __syncthreads();
+        if (!active) return;
 #pragma unroll
         for (int i = 0; i < NRT; ++i) {
             ev[i] = h3_vexp(fmaxf(fmaxf(red[4 * i], red[4 * i + 1]), fmaxf(red[4 * i + 2], red[4 * i + 3])));
@@ -579,12 +583,13 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
 }
 
 // Y = epi(X W^T + b) over a PTT-point tile (PTT/32 row tiles) by 4 waves.
-template <int IN, int OUT, int EPI, int PTT, bool F32>
+template <int IN, int OUT, int EPI, int PTT, bool F32, int NWV = 4>
 PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, const DenseOff &off, float *Y,
                       int ystr, const float *__restrict__ resid, int wave, int lane) {
     constexpr int NCT = OUT / 32, NRT = PTT / 32;
+    static_assert(NWV == 4 || NRT == 1, "8-wave workgroups take 32-point tiles");
     if constexpr (NCT >= 4) {
-        for (int ct = wave; ct < NCT; ct += 4)
+        for (int ct = wave; ct < NCT; ct += NWV)
             dense_tile<IN, OUT, EPI, NRT, F32>(X, xstr, pk, off, 0, ct, Y, ystr, resid, lane);
     } else if constexpr (NRT == 2) {
         const int rt = wave & 1, ct = wave >> 1;
@@ -595,9 +600,9 @@ PDSC_DEV void dense64(const float *X, int xstr, const float *__restrict__ pk, co
 }
 
 // Copy a [PT][CH] LDS tile (stride xstr) to global rows [p0, p0 + nrows) (row stride CH).
-template <int PTT>
+template <int PTT, int NT = 256>
 PDSC_DEV void store_rows(const float *X, int xstr, float *__restrict__ dst, int p0, int nrows, int tid) {
-    for (int e = tid; e < PTT * (CH / 4); e += 256) {
+    for (int e = tid; e < PTT * (CH / 4); e += NT) {
         const int p = e / (CH / 4), c4 = e % (CH / 4);
         if (p < nrows)
             *reinterpret_cast<f32x4 *>(dst + (size_t)(p0 + p) * CH + 4 * c4) =
@@ -663,6 +668,45 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
     }
 }
 
+// pcn_qkv for 8-wave workgroups (H3, 32-point tiles; small batches): PointCN on
+// waves 0-3, then Q (waves 0-3) and K (waves 4-7) at once, then V (waves 0-3).
+// Every output tile is the same dense_tile_w / dense_split code as the 4-wave
+// form, so the same bits.
+template <int PTT>
+PDSC_DEV void pcn_qkv8(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
+                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
+                       _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane) {
+    static_assert(PTT == 32, "8-wave chain: 32-point tiles");
+    const int w4 = wave & 3;
+    const bool lo = wave < 4;
+    WPanel<CH, false> pa, pb;
+    if (lo) {
+        load_wpanel<CH, CH, false>(pk, d.pcn, w4, lane, pa);
+        load_wpanel<CH, CH, false>(pk, d.q, w4, lane, pb);
+    } else {
+        load_wpanel<CH, CH, false>(pk, d.k, w4, lane, pb);
+    }
+    asm volatile("" ::: "memory");
+    if (lo) dense_tile_w<CH, CH, EPI_BN_RELU, 1, false>(Xin, S132, pa, pk, d.pcn, 0, w4, Xout, S132, nullptr, lane);
+    __syncthreads();  // Xout complete; Xin is dead (it now holds the split copy of Xout)
+    CH_STAMP(155);
+    char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
+    split_tile<PTT, 512>(Xout, S132, Xs, tid);
+    if (lo) load_wpanel<CH, CH, false>(pk, d.v, w4, lane, pa);
+    asm volatile("" ::: "memory");
+    store_rows<PTT, 512>(Xout, S132, feat, p0, PTT, tid);
+    __syncthreads();
+    CH_STAMP(156);
+    CH_STAMP(157);  // (Q and K run at once: the "k" phase of tools/pw_stamps.py)
+    if (lo)
+        dense_split<SPLIT_Q, 1>(Xs, pb, pk, d.q, w4, Q, p0, lane);
+    else
+        dense_split<SPLIT_K, 1>(Xs, pb, pk, d.k, w4, K, p0, lane);
+    CH_STAMP(158);
+    dense_split<SPLIT_V, 1>(Xs, pa, pk, d.v, w4, V, p0, lane, Xout, vexp, lo);  // Xout is dead
+    CH_STAMP(159);
+}
+
 // layer0 (Conv1d in_dim -> 128, :54, :73) + PointCN_0 + QKV_0.
 template <int PTT, bool F32>
 __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restrict__ pk, size_t l0w,
@@ -721,22 +765,22 @@ PDSC_DEV void combine_tile(const float *__restrict__ opart, const float *__restr
 
 // fc_message + residual (:43-44): X = msg (A) -> C -> A (stride S68) -> R (B);
 // C may alias R: it is dead once fc3 has read it (barrier before fc6).
-template <int PTT, bool F32>
+template <int PTT, bool F32, int NWV = 4>
 PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restrict__ pk, const PwMsg &m,
                             const float *__restrict__ feat_rows, int wave, int lane) {
-    dense64<CH, CH2, EPI_BN_RELU, PTT, F32>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
+    dense64<CH, CH2, EPI_BN_RELU, PTT, F32, NWV>(A, S132, pk, m.fc0, C, S68, nullptr, wave, lane);
     __syncthreads();
     CH_STAMP(152);
-    dense64<CH2, CH2, EPI_BN_RELU, PTT, F32>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
+    dense64<CH2, CH2, EPI_BN_RELU, PTT, F32, NWV>(C, S68, pk, m.fc3, A, S68, nullptr, wave, lane);
     __syncthreads();
     CH_STAMP(153);
-    dense64<CH2, CH, EPI_RESID, PTT, F32>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
+    dense64<CH2, CH, EPI_RESID, PTT, F32, NWV>(A, S68, pk, m.fc6, R, S132, feat_rows, wave, lane);
     __syncthreads();
     CH_STAMP(154);
 }
 
-template <int PTT, bool F32>
-__global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
+template <int PTT, bool F32, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
                                                      int Npad, float *__restrict__ feat,
@@ -752,12 +796,16 @@ __global__ __launch_bounds__(256, 2) void pw_mid_kernel(const float *__restrict_
     ATT_RSTAMP(stp, 186);
     ATT_STAMP(stp, 150);
 #endif
-    combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
+    if (tid < 256) combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     ATT_STAMP(stp, 151);
-    message_resid<PTT, F32>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
-    pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+    message_resid<PTT, F32, NWV>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    if constexpr (NWV == 8)
+        pcn_qkv8<PTT>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                       vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
+    else
+        pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
+                          vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
     ATT_RSTAMP(stp, 187);
 }
 
@@ -1592,6 +1640,17 @@ static bool small_tiles(int B, int Npad) {
     return (long)B * (Npad / 64) < lim;
 }
 
+// 8-wave pw_mid workgroups (32 points each) when the launch has at most one
+// workgroup per CU (a single N = 1000 pair: 32): the chain's output tiles
+// spread over twice the waves (A/B knob PDSC_PW_WAVES=4: never).
+static bool pw_waves8(int B, int Npad) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_PW_WAVES");
+        return e && atoi(e) == 4;
+    }();
+    return !off && (long)B * (Npad / 32) <= 256;
+}
+
 // One launch of pointwise kernel K<PTT, F32> with PTT and F32 picked at run time.
 #define PW_LAUNCH(K, rows, ...)                                                                         \
     do {                                                                                                \
@@ -1634,6 +1693,12 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
         hipLaunchKernelGGL(pw2_mid_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
                            packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad,
                            feat, Q, K, V, vexp);
+        return hipGetLastError();
+    }
+    if (!f32 && pw_waves8(B, Npad)) {
+        hipLaunchKernelGGL((pw_mid_kernel<32, false, 8>), dim3(Npad / 32, B), dim3(512), pw_lds<32>(), s, packed,
+                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, Q,
+                           K, V, vexp);
         return hipGetLastError();
     }
     PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,

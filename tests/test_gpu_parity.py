@@ -331,6 +331,27 @@ def test_precombine_bit_identical(gpu_device, tmp_path):
             assert np.array_equal(v, ref[k]), (B, N, k)
 
 
+def test_pw_waves8_bit_identical(gpu_device, tmp_path):
+    """Tiny batches run pw_mid with 8-wave workgroups (the chain's output tiles
+    over twice the waves): the same bits as the 4-wave kernel (a child process
+    with PDSC_PW_WAVES=4), encoder and forward: a single pair and a 5-pair batch
+    with a padded tail."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for B, N in ((1, 1000), (5, 777)):
+        ours = _fusion_outputs(gpu_device, B, N)
+        out = tmp_path / f"w4_{B}_{N}.npz"
+        env = dict(os.environ, PDSC_PW_WAVES="4")
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = np.load(out)
+        for k, v in ours.items():
+            assert np.array_equal(v, ref[k]), (B, N, k)
+
+
 def test_graph_replay_equals_eager(gpu_device):
     """ForwardPlan.capture(): a HIP-graph replay of the forward gives the eager
     result bitwise, and picks up new contents of the same input buffers; the
