@@ -556,6 +556,27 @@ def test_local_max_bit_exact_random(radius, gpu_device):
         assert np.array_equal(lm[b], O.local_max(src[b], conf[b], radius)), b
 
 
+@pytest.mark.parametrize("B,N,S,zeros", [(3, 1000, 100, 0.0), (2, 5000, 500, 0.97), (1, 777, 77, 1.0),
+                                          (2, 9000, 900, 0.5), (1, 3000, 2999, 0.3)])
+def test_seed_ranking_ties(B, N, S, zeros, gpu_device):
+    """a5's ranking = argsort(score, descending) with ties by ascending index, on
+    scores with a fraction of exact zeros (non-maxima, +0 and -0), duplicates
+    and negatives.  radius 0: every point a local maximum, so the scores are the
+    confidences themselves."""
+    from pointdsc_amd import kernels
+    rng = np.random.RandomState(N + S)
+    src = rng.rand(B, N, 3).astype(np.float32)
+    conf = np.round(rng.randn(B, N), 2).astype(np.float32)  # many duplicates
+    z = rng.rand(B, N) < zeros
+    conf[z] = np.where(rng.rand(int(z.sum())) < 0.5, 0.0, -0.0).astype(np.float32)
+    seeds, lm = kernels.pick_seeds(_t(src, gpu_device), _t(conf, gpu_device), 0.0, S)
+    seeds = seeds.cpu().numpy()
+    assert lm.cpu().numpy().min() == 1.0
+    for b in range(B):
+        order = sorted(range(N), key=lambda i: (-float(conf[b, i]), i))[:S]
+        assert np.array_equal(seeds[b], np.array(order, np.int32)), b
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("N", [300, 2000, 5000, 9000])  # 9000: rows past the register variants (R = 0)
 def test_seed_knn_random(N, precision, gpu_device):
