@@ -225,11 +225,21 @@ int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float
     return PDSC_OK;
 }
 
+// A/B knob (measurement only): PDSC_RAGGED_ORDER=0 keeps the ragged attention
+// workgroups in pair order.
+static bool ragged_order_on() {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_RAGGED_ORDER");
+        return e && e[0] == '0';
+    }();
+    return !off;
+}
+
 struct FwdBufs {
     float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights, *hsums;
     _Float16 *normed_s;
     int *seeds, *knn, *counts;
-    int *nv, *sv;  // ragged batches: per-pair correspondences and seeds
+    int *nv, *sv, *po;  // ragged batches: per-pair correspondences and seeds, attention pair order
     EncBufs enc;
     NsmBufs nsm;
 };
@@ -253,6 +263,7 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.hsums = c.take<float>((size_t)d.B * d.S * 15);
     f.nv = c.take<int>((size_t)d.B);
     f.sv = c.take<int>((size_t)d.B);
+    f.po = c.take<int>((size_t)d.B);
     return f;
 }
 
@@ -653,6 +664,10 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
         HIPCHK(launch_ragged_setup(counts, B, cfg->ratio, f.nv, f.sv, s));
         rg.nv = f.nv;
         rg.sv = f.sv;
+        if (ragged_order_on()) {
+            HIPCHK(launch_ragged_order(counts, B, f.po, s));
+            rg.po = f.po;
+        }
     }
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
     const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;

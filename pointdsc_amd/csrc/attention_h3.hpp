@@ -257,6 +257,7 @@ struct AttnGridH3 {
     int B, N, Npad, nqb, nsplit, sps;  // sps = 32-key tiles per split
     // ragged batches: pair b's correspondences (N, Npad: the batch's strides), or null
     const int *nv;
+    const int *po;  // ragged batches: workgroup pair slot -> pair (Ragged::po), or null
     PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
@@ -289,6 +290,7 @@ template <int NW>
 inline AttnGridH3 attention_h3_grid(int B, int N, int slots) {
     AttnGridH3 g;
     g.nv = nullptr;
+    g.po = nullptr;
     g.B = B;
     g.N = N;
     g.Npad = round_up(N, QB);
@@ -312,7 +314,8 @@ PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
         const int full = G & ~7;
         if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
     }
-    return AttnBlock{lid / g.nsplit / g.nqb, (lid / g.nsplit) % g.nqb, lid % g.nsplit};
+    const int slot = lid / g.nsplit / g.nqb;
+    return AttnBlock{g.po ? g.po[slot] : slot, (lid / g.nsplit) % g.nqb, lid % g.nsplit};
 }
 
 // The attention of one workgroup (NW waves x 32 queries of pair b, query block

@@ -12,6 +12,7 @@
 // ops), so computing each pair once halves the VALU work that would otherwise
 // sit right at the write roofline.  Stores are 16 B per lane.
 #include <algorithm>
+#include <vector>
 
 #include "pdsc_internal.hpp"
 
@@ -293,6 +294,39 @@ hipError_t launch_ragged_setup(const int32_t *counts, int B, double ratio, int *
         const int nb = std::min(RAGGED_CHUNK, B - b0);
         for (int i = 0; i < nb; ++i) c.n[i] = counts[b0 + i];
         hipLaunchKernelGGL(ragged_setup_kernel, dim3(1), dim3(RAGGED_CHUNK), 0, s, c, nb, ratio, nv + b0, sv + b0);
+        HIP_RET(hipGetLastError());
+    }
+    return hipSuccess;
+}
+
+__global__ void ragged_order_kernel(RaggedChunk c, int nb, int *__restrict__ po) {
+    const int i = threadIdx.x;
+    if (i < nb) po[i] = c.n[i];
+}
+
+hipError_t launch_ragged_order(const int32_t *counts, int B, int *po, hipStream_t s) {
+    std::vector<int> rank(B), order(B), next(8), end(8);
+    for (int b = 0; b < B; ++b) rank[b] = b;
+    std::stable_sort(rank.begin(), rank.end(), [&](int a, int b) { return counts[a] > counts[b]; });
+    // the slot ranges of the 8 XCDs (attention_h3_block: consecutive workgroup
+    // ids round-robin over the XCDs, each XCD's logical ids contiguous)
+    for (int x = 0; x < 8; ++x) {
+        next[x] = (int)((long)B * x / 8);
+        end[x] = (int)((long)B * (x + 1) / 8);
+    }
+    std::vector<double> load(8, 0.0);
+    for (int r = 0; r < B; ++r) {
+        int best = -1;
+        for (int x = 0; x < 8; ++x)
+            if (next[x] < end[x] && (best < 0 || load[x] < load[best])) best = x;
+        order[next[best]++] = rank[r];
+        load[best] += (double)counts[rank[r]] * counts[rank[r]];
+    }
+    for (int b0 = 0; b0 < B; b0 += RAGGED_CHUNK) {
+        RaggedChunk c{};
+        const int nb = std::min(RAGGED_CHUNK, B - b0);
+        for (int i = 0; i < nb; ++i) c.n[i] = order[b0 + i];
+        hipLaunchKernelGGL(ragged_order_kernel, dim3(1), dim3(RAGGED_CHUNK), 0, s, c, nb, po + b0);
         HIP_RET(hipGetLastError());
     }
     return hipSuccess;

@@ -165,6 +165,7 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
                    *vs = static_cast<const _Float16 *>(v);
     AttnGridH3 g = prod_grid(B, N);
     g.nv = rg.nv;
+    g.po = rg.po;
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     if (m_packed)
         hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), dim3(g.B * g.nqb * g.nsplit),
@@ -1589,6 +1590,7 @@ hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer
                            float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s, Ragged rg) {
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
+    g.po = rg.po;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
     const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
     const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
@@ -1610,6 +1612,7 @@ hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, cons
                                 float *conf, hipStream_t s, Ragged rg) {
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
+    g.po = rg.po;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad) return hipErrorInvalidValue;
     W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
     w2_sched_add(S, lay.c0, CH, CLS);

@@ -126,6 +126,8 @@ inline PackLayout make_layout(int L, int in_dim) {
 // largest).  nv == sv == nullptr: a uniform batch (every pair N rows, S seeds).
 struct Ragged {
     const int *nv = nullptr, *sv = nullptr;
+    // the attention's pair order (longest pairs first, dealt over the XCDs), or null
+    const int *po = nullptr;
     PDSC_DEV int n(int b, int N) const { return nv ? nv[b] : N; }
     PDSC_DEV int s(int b, int S) const { return sv ? sv[b] : S; }
 };
@@ -133,6 +135,11 @@ constexpr int RAGGED_CHUNK = 512;  // counts per setup launch (kernel-argument a
 // counts (HOST, already validated) -> nv [B], sv [B] on the device, through
 // kernel arguments (no host-to-device copy of pageable memory on the stream)
 hipError_t launch_ragged_setup(const int32_t *counts_host, int B, double ratio, int *nv, int *sv, hipStream_t s);
+// counts (HOST) -> po [B]: attention workgroup slot -> pair, so the workgroups
+// of the largest pairs start first (each XCD's slots in decreasing pair size,
+// pairs dealt to the XCD with the least N^2 so far): list scheduling of
+// workgroups of unequal length, longest first
+hipError_t launch_ragged_order(const int32_t *counts_host, int B, int *po, hipStream_t s);
 
 // ---- launchers --------------------------------------------------------------
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
