@@ -59,7 +59,7 @@ enum pdsc_precision {
 
 /* Hyper-parameters of PointDSC.__init__ (models/PointDSC.py:81-100). */
 typedef struct pdsc_config {
-    int32_t in_dim;           /* 6 */
+    int32_t in_dim;           /* 6 (1 .. 128; the reference's 6, 9, 12, 70) */
     int32_t num_layers;       /* 12 in both release configs */
     int32_t num_channels;     /* 128 (the only width the HIP kernels implement) */
     int32_t num_iterations;   /* power-iteration cap, 10 */

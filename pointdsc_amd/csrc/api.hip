@@ -71,7 +71,7 @@ int check_cfg(const pdsc_config *cfg) {
         return fail(PDSC_ERR_UNSUPPORTED, "num_channels=%d: only %d is implemented", cfg->num_channels, CH);
     if (cfg->num_layers < 1 || cfg->num_layers > 64)
         return fail(PDSC_ERR_UNSUPPORTED, "num_layers=%d not in [1, 64]", cfg->num_layers);
-    if (cfg->in_dim < 1 || cfg->in_dim > 16) return fail(PDSC_ERR_UNSUPPORTED, "in_dim=%d not in [1, 16]", cfg->in_dim);
+    if (cfg->in_dim < 1 || cfg->in_dim > 128) return fail(PDSC_ERR_UNSUPPORTED, "in_dim=%d not in [1, 128]", cfg->in_dim);
     if (cfg->num_iterations < 0 || cfg->num_iterations > 31)
         return fail(PDSC_ERR_UNSUPPORTED, "num_iterations=%d not in [0, 31]", cfg->num_iterations);
     if (cfg->k < 1) return fail(PDSC_ERR_ARG, "k=%d", cfg->k);

@@ -356,7 +356,8 @@ hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int N
 enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
 
 constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
-constexpr int IN_MAX = 16;  // layer0 input width held in registers
+constexpr int IN_MAX = 16;     // layer0 input width held in registers (pw_first)
+constexpr int IN_LIMIT = 128;  // layer0 input width supported (datasets/ThreeDMatch.py:311-315: 70)
 
 // The wave's weight panel for output tile ct.  H3: per 16-input k-step, the hi
 // and lo fragments (lane (h, n): inputs 16 ks + 8h .. +7 of output 32 ct + n).
@@ -729,17 +730,27 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
     }
     // thread -> output channel j (both halves of the block cover rows of opposite parity)
     const int j = tid & (CH - 1), p_off = tid >> 7;
-    float w[IN_MAX];
-#pragma unroll
-    for (int c = 0; c < IN_MAX; ++c) w[c] = (c < in_dim) ? pk[l0w + j * in_dim + c] : 0.0f;
     const float bj = pk[l0b + j];
-    __syncthreads();
-    for (int p = p_off; p < PTT; p += 2) {
-        float s = 0.0f;
+    if (in_dim <= IN_MAX) {  // the weights in registers
+        float w[IN_MAX];
 #pragma unroll
-        for (int c = 0; c < IN_MAX; ++c)
-            if (c < in_dim) s = __builtin_fmaf(w[c], cp[p * in_dim + c], s);
-        XA[p * S132 + j] = s + bj;
+        for (int c = 0; c < IN_MAX; ++c) w[c] = (c < in_dim) ? pk[l0w + j * in_dim + c] : 0.0f;
+        __syncthreads();
+        for (int p = p_off; p < PTT; p += 2) {
+            float s = 0.0f;
+#pragma unroll
+            for (int c = 0; c < IN_MAX; ++c)
+                if (c < in_dim) s = __builtin_fmaf(w[c], cp[p * in_dim + c], s);
+            XA[p * S132 + j] = s + bj;
+        }
+    } else {  // wide inputs (in_dim <= IN_LIMIT): the same ascending fma chain, weights from L1
+        __syncthreads();
+        const float *wj = pk + l0w + (size_t)j * in_dim;
+        for (int p = p_off; p < PTT; p += 2) {
+            float s = 0.0f;
+            for (int c = 0; c < in_dim; ++c) s = __builtin_fmaf(wj[c], cp[p * in_dim + c], s);
+            XA[p * S132 + j] = s + bj;
+        }
     }
     __syncthreads();
     pcn_qkv<PTT, F32>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
@@ -1673,7 +1684,7 @@ static bool pw_waves8(int B, int Npad) {
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
                            int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
                            Ragged rg) {
-    if (lay.in_dim > IN_MAX) return hipErrorInvalidValue;
+    if (lay.in_dim > IN_LIMIT) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
         const W2Sched S = sched_qkv(W2Sched{}, dense4(lay.layer[0]));

@@ -108,6 +108,49 @@ def test_encoder_and_classifier(name, precision, gpu_device):
     assert np.abs(normed[0].double().cpu().numpy() - n64).max() <= 2 * rel_row + 1e-6
 
 
+@pytest.mark.parametrize("in_dim", [9, 70])
+@pytest.mark.parametrize("B", [1, 40])  # pw_first (LDS-tiled) and pw2_first (register-chained) layer0
+def test_wide_layer0_inputs(in_dim, B, gpu_device):
+    """in_dim = 70 (corr_pos + both FPFH descriptors, datasets/ThreeDMatch.py:311-315)
+    and 9: layer0 wider than the 16 inputs held in registers.  A synthetic case
+    (parity unpinned: no reference output for these widths): rel_1k's geometry,
+    its trained weights with layer0 replaced by a random in_dim one, descriptor
+    columns of FPFH-like magnitude; features and logits within ENVELOPE x the
+    network's own fp32 noise (conftest.encoder_torch realisations) of fp64."""
+    from conftest import FP32_REALISATIONS, encoder_fp64, encoder_torch
+    from pointdsc_amd import kernels
+    from pointdsc_amd.PointDSC import PointDSC
+    g = dict(load_golden("rel_1k"))
+    rng = np.random.RandomState(in_dim)
+    N = g["corr_pos"].shape[0]
+    extra = (rng.rand(N, in_dim - 6) * 0.2).astype(np.float32)
+    g["corr_pos"] = np.ascontiguousarray(np.concatenate([g["corr_pos"], extra], 1).astype(np.float32))
+    sd = dict(golden_state_dict(g))
+    sd["encoder.layer0.weight"] = (rng.randn(128, in_dim, 1) / np.sqrt(in_dim)).astype(np.float32)
+    hp = golden_hparams(g)
+    m = PointDSC(in_dim=in_dim, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
+                 nms_radius=hp["nms_radius"])
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to(gpu_device).eval()
+    f64, c64 = encoder_fp64(g, sd, gpu_device)
+    mx = np.abs(f64).max()
+    e_f = e_c = 0.0
+    for s in range(FP32_REALISATIONS):
+        f32, c32 = encoder_torch(g, sd, gpu_device, torch.float32, seed=s)
+        e_f = max(e_f, np.abs(f32 - f64).max() / mx)
+        e_c = max(e_c, np.abs(c32 - c64).max())
+    rep = lambda a: _t(np.repeat(a[None], B, 0), gpu_device)
+    corr, src, tgt = rep(g["corr_pos"]), rep(g["src_keypts"]), rep(g["tgt_keypts"])
+    M = kernels.compat(src, tgt, m.sigma_spat)
+    feat, _, conf = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, M)
+    for b in (0, B - 1):
+        ours_f = np.abs(feat[b].double().cpu().numpy() - f64).max() / mx
+        ours_c = np.abs(conf[b].double().cpu().numpy() - c64).max()
+        assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (b, ours_f, e_f)
+        assert ours_c <= ENVELOPE * e_c + LOGIT_FLOOR, (b, ours_c, e_c)
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_h3_matches_exact_fp32(name, gpu_device):
     """The 3xfp16 contractions against the exact-fp32 MFMA mode on the same inputs:
