@@ -1303,6 +1303,10 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_first_kernel(const fl
                                                                  _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                                  _Float16 *__restrict__ V, float *__restrict__ vexp,
                                                                  const int *__restrict__ nv) {
+    // ragged batches: a workgroup wholly past its pair's rows has nothing any later
+    // kernel reads (the attention's key tiles end at round_up(n, 32) <= its first
+    // row; its query blocks past n exit) -- leave before staging any weights
+    if (nv && (int)blockIdx.x * PW2_PTS >= nv[blockIdx.y]) return;  // workgroup-uniform
     PW2_PROLOGUE
     const int l32 = lane & 31;
     const int n = nv ? nv[b] : N;  // this pair's rows (ragged batches); N: the row stride
