@@ -358,10 +358,15 @@ def main():
         _lib.check(L.pdsc_attention_layout(P, N, 0, ctypes.byref(npad), ctypes.byref(nsplit)), "attention_layout")
         _lib.check(L.pdsc_encoder_plan(P, N, 0, ctypes.byref(fused)), "encoder_plan")
         grid = P * (npad.value // 128) * nsplit.value * 256
-        if fused.value:
+        if fused.value == 2:  # the split path's 64-query-wave attention (one 256-query workgroup per CU)
+            grid = P * ((N + 255) // 256) * nsplit.value * 256
+        if fused.value == 1:
             # attention 4 N^2 C + chain 2 x (fc0 128x64 + fc3 64x64 + fc6 64x128 + PointCN/Q/K/V 4 x 128x128) per point
             flops = P * (4.0 * N * N * 128 + 2.0 * 86016 * N)
             kname, kdesc, n_launch = "attn_pw2_kernel<1>", "attn_pw2_kernel (attention_l + pointwise chain_l, packed M)", 11
+        elif fused.value == 2:
+            flops = P * 4.0 * N * N * 128
+            kname, kdesc, n_launch = "attention_w64_kernel", "attention_w64_kernel<xcd> (64-query waves, fragment-ordered M)", 12
         else:
             flops = P * 4.0 * N * N * 128
             kname, kdesc, n_launch = "attention_h3_kernel<4>", "attention_h3_kernel<4,xcd>", 12

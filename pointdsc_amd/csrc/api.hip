@@ -65,6 +65,12 @@ bool dense_m_requested() {
     return v;
 }
 
+// The forward's M layout: fragment-ordered where the split path runs attention_w64,
+// symmetric-packed for the other H3 plans, dense for exact fp32 (and PDSC_DENSE_M=1
+// on the h3 plans, measurement only).
+struct Dims;
+int forward_m_layout(const Dims &d);
+
 int check_cfg(const pdsc_config *cfg) {
     if (!cfg) return fail(PDSC_ERR_ARG, "cfg is NULL");
     if (cfg->num_channels != CH)
@@ -97,6 +103,7 @@ struct Dims {
     int B, N, Npad, S, k, T, nsplit;
     bool f32;   // PDSC_PRECISION_F32
     bool fuse;  // attention + pointwise chain in one launch per layer (attention_fused)
+    bool w64;   // split path with attention_w64 (fragment-ordered M)
     bool precombine;  // split partials combined by combine_rows ahead of the pointwise kernels
 };
 
@@ -110,12 +117,18 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
     d.k = std::min(cfg->k, N - 1);        // (:250)
     d.T = cfg->num_iterations;
     d.f32 = cfg->precision == PDSC_PRECISION_F32;
-    d.nsplit = attention_nsplit(B, N, d.f32);
     d.fuse = attention_fused(B, N, d.f32);
+    d.w64 = !d.fuse && attention_w64(B, N, d.f32);
+    d.nsplit = attention_nsplit(B, N, d.f32, d.w64);
     d.precombine = use_precombine(B, d.Npad, d.nsplit, d.f32, d.fuse);
     if (d.S < 1) return fail(PDSC_ERR_ARG, "int(N*ratio) = 0 seeds for N=%d", N);
     if (d.k > 63) return fail(PDSC_ERR_UNSUPPORTED, "k=%d > 63", d.k);
     return PDSC_OK;
+}
+
+int forward_m_layout(const Dims &d) {
+    if (d.w64) return M_FRAG;
+    return (!dense_m_requested() && !d.f32) ? M_PACKED : M_DENSE;
 }
 
 struct EncBufs {
@@ -149,8 +162,10 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
 }
 
 int run_encoder(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
-                bool m_packed, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
+                int m_layout, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s, Ragged rg = {}) {
+    const bool m_packed = m_layout == M_PACKED;
+    if ((m_layout == M_FRAG) != (d.w64 && !d.fuse)) return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg));
     if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
@@ -173,7 +188,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
-        HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_packed, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
+        HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_layout, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
                                 s, rg));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         const float *op = e.opart, *mlp = e.ml;
@@ -247,7 +262,7 @@ struct FwdBufs {
 FwdBufs carve_forward(Carve &c, const Dims &d) {
     FwdBufs f;
     // symmetric-packed tiles (PDSC_DENSE_M=1: the dense [N][N] form, for A/B measurement)
-    f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), (size_t)d.N * d.N));
+    f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), mfrag_floats(d.N)));  // (mfrag >= N^2: dense fits)
     f.enc = carve_encoder(c, d);
     f.normed = c.take<float>((size_t)d.B * d.N * CH);
     f.normed_s = c.take<_Float16>((size_t)d.B * d.N * 2 * CH);
@@ -388,6 +403,15 @@ int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N
 }
 
 size_t pdsc_compat_packed_floats(int32_t N) { return N < 1 ? 0 : mpack_floats(N); }
+size_t pdsc_compat_frag_floats(int32_t N) { return N < 1 ? 0 : mfrag_floats(N); }
+
+int32_t pdsc_compat_frag_f32(const float *src, const float *tgt, int32_t B, int32_t N, const float *sigma_d_dev,
+                             float *Mf, pdsc_stream_t stream) {
+    if (!src || !tgt || !sigma_d_dev || !Mf) return fail(PDSC_ERR_ARG, "null pointer");
+    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
+    HIPCHK(launch_compat_frag(src, tgt, B, N, sigma_d_dev, Mf, S_(stream)));
+    return PDSC_OK;
+}
 
 int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                                const float *sigma_d_dev, float *Mp, pdsc_stream_t stream) {
@@ -398,9 +422,17 @@ int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, in
 }
 
 // ---------------------------------------------------------------- a2-a4
+// the standalone encoder takes the caller's dense M: its plan never runs attention_w64
+static void dims_dense_m(Dims &d) {
+    d.w64 = false;
+    d.nsplit = attention_nsplit(d.B, d.N, d.f32, false);
+    d.precombine = use_precombine(d.B, d.Npad, d.nsplit, d.f32, d.fuse);
+}
+
 size_t pdsc_encoder_workspace_bytes(const pdsc_config *cfg, int32_t B, int32_t N) {
     Dims d;
     if (check_cfg(cfg) != PDSC_OK || make_dims(cfg, B, N, d) != PDSC_OK) return 0;
+    dims_dense_m(d);
     Carve c(nullptr);
     carve_encoder(c, d);
     return c.off;
@@ -412,12 +444,13 @@ int32_t pdsc_encoder_f32(const pdsc_config *cfg, const float *packed, const floa
     RET_IF(check_cfg(cfg));
     Dims d;
     RET_IF(make_dims(cfg, B, N, d));
+    dims_dense_m(d);
     if (!packed || !corr_pos || !M || !normed || !conf || !ws) return fail(PDSC_ERR_ARG, "null pointer");
     RET_IF(need_ws(ws_bytes, pdsc_encoder_workspace_bytes(cfg, B, N)));
     Carve c(ws);
     const EncBufs e = carve_encoder(c, d);
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
-    return run_encoder(lay, packed, corr_pos, M, false, d, e, feat, normed, nullptr, conf, S_(stream));
+    return run_encoder(lay, packed, corr_pos, M, M_DENSE, d, e, feat, normed, nullptr, conf, S_(stream));
 }
 
 size_t pdsc_attention_workspace_bytes(int32_t B, int32_t N, int32_t C, int32_t precision) {
@@ -457,7 +490,7 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     } else {  // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
         HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, vexp, s));
     }
-    HIPCHK(launch_attention(qs, ks, vs, vexp, M, false, f32, B, N, Npad, ns, op, ml, s));
+    HIPCHK(launch_attention(qs, ks, vs, vexp, M, M_DENSE, f32, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, f32, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
@@ -486,7 +519,8 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *
         return fail(PDSC_ERR_ARG, "precision %d (enum pdsc_precision)", precision);
     if (B < 1 || N < 1 || !Npad || !nsplit) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
     *Npad = round_up(N, QB);
-    *nsplit = attention_nsplit(B, N, precision == PDSC_PRECISION_F32);
+    const bool f32 = precision == PDSC_PRECISION_F32;
+    *nsplit = attention_nsplit(B, N, f32, !attention_fused(B, N, f32) && attention_w64(B, N, f32));
     return PDSC_OK;
 }
 
@@ -494,7 +528,8 @@ int32_t pdsc_encoder_plan(int32_t B, int32_t N, int32_t precision, int32_t *fuse
     if (precision != PDSC_PRECISION_H3 && precision != PDSC_PRECISION_F32)
         return fail(PDSC_ERR_ARG, "precision %d (enum pdsc_precision)", precision);
     if (B < 1 || N < 1 || !fused) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
-    *fused = attention_fused(B, N, precision == PDSC_PRECISION_F32) ? 1 : 0;
+    const bool f32 = precision == PDSC_PRECISION_F32, fu = attention_fused(B, N, f32);
+    *fused = fu ? 1 : (attention_w64(B, N, f32) ? 2 : 0);
     return PDSC_OK;
 }
 
@@ -678,14 +713,16 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     if (ev) HIPCHK(hipEventRecord(ev[i], s))
     STAGE(0);
     // a1 (:150-153)
-    const bool mpacked = !dense_m_requested() && !d.f32;  // the exact-fp32 attention reads dense M
-    if (mpacked)
+    const int mlay = forward_m_layout(d);
+    if (mlay == M_FRAG)
+        HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
+    else if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s, rg));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mlay, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s, rg));
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s, rg));
@@ -757,12 +794,14 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);
     const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
     // a1-a4 as in testing (:150-156, :171)
-    const bool mpacked = !dense_m_requested() && !d.f32;
-    if (mpacked)
+    const int mlay = forward_m_layout(d);
+    if (mlay == M_FRAG)
+        HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s));
+    else if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mpacked, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
+    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mlay, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s));
     // the loss's feature-similarity M (:158-163)
     if (M_out)
         HIPCHK(launch_feat_sim(d.f32 ? static_cast<const void *>(f.normed) : static_cast<const void *>(f.normed_s),

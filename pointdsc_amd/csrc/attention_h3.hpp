@@ -21,6 +21,12 @@
 // [0, H3_VEXP_MAX], chosen by the producer from the tile's max |v|) so its lo
 // halves stay normal fp16; the tile's p are formed as 2^(x - m + PSHIFT - e)
 // (one add) and its sum re-scaled by 2^e (one ldexp): sum p v is unchanged.
+// The scale trades V's resolution against p's: both halves bottom out at fp16's
+// 2^-24, V' relative to the tile's max 2^(e + log2 max|v|), p' relative to the
+// row sum >= 2^(PSHIFT - e).  e lifts max|v'| only to [2^4, 2^5): a larger e
+// (r03: max|v'| up to 2^14, e = 8 for any |v| < 64) pushed the p' of keys far
+// below the row max under 2^-24 -- lost mass that grows with the key chain,
+// measured 5x the fp32 envelope at one 1000-key split (tools/emulate_attn.py).
 // Small Q or K only shrink the logits' absolute error, which is what the
 // softmax is sensitive to.
 //
@@ -75,15 +81,16 @@ constexpr float H3_DEFER = 8.0f;             // re-base the max when it grows by
 #define ATT_BUFDMA 1  // K/V (and pw2 weight) LDS-DMA by buffer_load ... lds (no per-piece 64-bit address VALU)
 #endif
 constexpr float H3_QSCALE = 0.12751743082459868f;  // log2(e) / sqrt(128): the softmax's scale, in base 2
-constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8 (p * 2^-e stays >= 2^-24 of the sum)
+constexpr int H3_VEXP_MAX = 8;               // V tile pre-scale 2^e, 0 <= e <= 8
+constexpr int H3_VEXP_TARGET = 5;            // ... lifting the tile's max |v| below 2^5
 
 // The V-tile exponent for a tile whose max |v| is vmax: the largest e <= 8 with
-// vmax 2^e < 2^14 (0 for vmax >= 2^13, vmax == 0 or non-finite vmax).
+// vmax 2^e < 2^H3_VEXP_TARGET (0 for vmax >= 2^4, vmax == 0 or non-finite vmax).
 PDSC_DEV int h3_vexp(float vmax) {
     if (!(vmax > 0.0f) || !(vmax < 8192.0f)) return 0;
     int ex;
     frexpf(vmax, &ex);  // vmax < 2^ex
-    return max(0, min(H3_VEXP_MAX, 14 - ex));
+    return max(0, min(H3_VEXP_MAX, H3_VEXP_TARGET - ex));
 }
 
 // channel -> position in a Qs/Ks row: swap bits 2 and 3

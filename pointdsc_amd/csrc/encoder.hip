@@ -26,6 +26,7 @@
 
 #include "attention.hpp"
 #include "attention_h3.hpp"
+#include "attention_w64.hpp"
 
 namespace pdsc {
 
@@ -145,11 +146,39 @@ static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, 
 constexpr int ATT_F32_KTS = 32;
 static AttnGrid f32_grid(int B, int N) { return attention_grid<ATT_NW, ATT_F32_KTS>(B, N, att_target()); }
 
-int attention_nsplit(int B, int N, bool f32) { return f32 ? f32_grid(B, N).nsplit : prod_grid(B, N).nsplit; }
+// The 64-query-wave attention (attention_w64.hpp, one 4-wave workgroup per CU,
+// fragment-ordered M) for the split path: from 128 blocks of 256 queries
+// (8 x 5000: 160 blocks, 3 key splits).  Knob PDSC_W64: 0 never, 1 wherever the
+// split path runs (measurement only).
+static AttnGridH3 w64_grid(int B, int N) { return attention_w64_grid(B, N, att_target() / 2); }
+bool attention_w64(int B, int N, bool f32) {
+    static const int mode = [] {
+        const char *e = getenv("PDSC_W64");
+        return e ? atoi(e) : 2;
+    }();
+    if (f32 || mode == 0) return false;
+    return mode == 1 || (long)B * ((N + W64_QPB - 1) / W64_QPB) >= 128;
+}
+
+int attention_nsplit(int B, int N, bool f32, bool w64) {
+    return f32 ? f32_grid(B, N).nsplit : (w64 ? w64_grid(B, N).nsplit : prod_grid(B, N).nsplit);
+}
 
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
-                            bool m_packed, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
+                            int m_layout, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s, Ragged rg) {
+    const bool m_packed = m_layout == M_PACKED;
+    if (m_layout == M_FRAG) {  // attention_w64 (H3 layouts, fragment-ordered M)
+        if (f32) return hipErrorInvalidValue;
+        AttnGridH3 g = w64_grid(B, N);
+        g.nv = rg.nv;
+        g.po = rg.po;
+        if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((attention_w64_kernel<true>), dim3(g.B * g.nqb * g.nsplit), dim3(W64_NW * 64), W64_LDS, s,
+                           static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
+                           static_cast<const _Float16 *>(v), vexp, M, g, opart, ml);
+        return hipGetLastError();
+    }
     if (f32) {  // fp32 [B][Npad][CH] rows, dense M
         AttnGrid g = f32_grid(B, N);
         g.nv = rg.nv;

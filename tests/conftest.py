@@ -29,13 +29,17 @@ def load_golden(name):
 def golden_state_dict(g):
     """The exact state dict a golden case was generated with (see tools/gen_goldens.py)."""
     from pointdsc_amd.synthetic import trained_state_dict
-    return trained_state_dict(str(g["preset"]), int(g["num_layers"]), float(g["cls_bias_shift"]),
-                              float(g["cls_scale"]))
+    sd = trained_state_dict(str(g["preset"]), int(g["num_layers"]), float(g["cls_bias_shift"]),
+                            float(g["cls_scale"]))
+    if "layer0_weight" in g:  # wide layer-0 inputs (in_dim 9 / 70): the case's own layer0
+        sd["encoder.layer0.weight"] = np.asarray(g["layer0_weight"], np.float32)
+    return sd
 
 
 def golden_hparams(g):
     return dict(num_layers=int(g["num_layers"]), inlier_threshold=float(g["inlier_threshold"]),
-                nms_radius=float(g["nms_radius"]), num_iterations=10, ratio=0.1, k=40)
+                nms_radius=float(g["nms_radius"]), num_iterations=10, ratio=0.1, k=40,
+                in_dim=int(g["in_dim"]) if "in_dim" in g else 6)
 
 
 def assert_close_scaled(actual, desired, rel=5e-5):

@@ -37,7 +37,7 @@ def _t(x, dev, dtype=torch.float32):
 def _model(g, dev, precision="h3"):
     from pointdsc_amd.PointDSC import PointDSC
     hp = golden_hparams(g)
-    m = PointDSC(in_dim=6, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
+    m = PointDSC(in_dim=hp["in_dim"], num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
                  inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
                  nms_radius=hp["nms_radius"], precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state_dict(g).items()})
@@ -74,6 +74,9 @@ def test_compat(name, gpu_device):
     M = kernels.compat(src, tgt, sd)[0]
     if "M" in g:
         assert np.array_equal(M.cpu().numpy(), g["M"])  # bit-exact
+    # the forward's two layouts hold the same bits (packed; fragment-ordered)
+    assert torch.equal(kernels.compat_packed(src, tgt, sd)[0], M)
+    assert torch.equal(kernels.compat_frag(src, tgt, sd)[0], M)
     assert np.array_equal(torch.diagonal(M).cpu().numpy(), g["M_diag"])
     assert torch.equal(M, M.T)
     np.testing.assert_allclose(M.double().sum(-1).cpu().numpy(), g["M_row_sums"], rtol=1e-12, atol=1e-9)
@@ -108,38 +111,20 @@ def test_encoder_and_classifier(name, precision, gpu_device):
     assert np.abs(normed[0].double().cpu().numpy() - n64).max() <= 2 * rel_row + 1e-6
 
 
-@pytest.mark.parametrize("in_dim", [9, 70])
+@pytest.mark.parametrize("name", ["wide9_1k", "wide70_1k"])
 @pytest.mark.parametrize("B", [1, 40])  # pw_first (LDS-tiled) and pw2_first (register-chained) layer0
-def test_wide_layer0_inputs(in_dim, B, gpu_device):
-    """in_dim = 70 (corr_pos + both FPFH descriptors, datasets/ThreeDMatch.py:311-315)
-    and 9: layer0 wider than the 16 inputs held in registers.  A synthetic case
-    (parity unpinned: no reference output for these widths): rel_1k's geometry,
-    its trained weights with layer0 replaced by a random in_dim one, descriptor
-    columns of FPFH-like magnitude; features and logits within ENVELOPE x the
-    network's own fp32 noise (conftest.encoder_torch realisations) of fp64."""
-    from conftest import FP32_REALISATIONS, encoder_fp64, encoder_torch
+def test_wide_layer0_inputs(name, B, gpu_device):
+    """in_dim = 70 (corr_pos + both 32-d descriptors, datasets/ThreeDMatch.py:311-315)
+    and 9 (:308-309): layer0 wider than the 16 inputs held in registers, against
+    the REFERENCE's own outputs for these widths (tools/gen_goldens.py runs
+    models/PointDSC.py with in_dim 9 / 70).  Single pairs and a 40-pair batch of
+    the same pair (the batched layer-0 kernel): features / logits in the fp32
+    envelope, labels and seeds as the reference, poses 1e-4."""
     from pointdsc_amd import kernels
-    from pointdsc_amd.PointDSC import PointDSC
-    g = dict(load_golden("rel_1k"))
-    rng = np.random.RandomState(in_dim)
-    N = g["corr_pos"].shape[0]
-    extra = (rng.rand(N, in_dim - 6) * 0.2).astype(np.float32)
-    g["corr_pos"] = np.ascontiguousarray(np.concatenate([g["corr_pos"], extra], 1).astype(np.float32))
-    sd = dict(golden_state_dict(g))
-    sd["encoder.layer0.weight"] = (rng.randn(128, in_dim, 1) / np.sqrt(in_dim)).astype(np.float32)
-    hp = golden_hparams(g)
-    m = PointDSC(in_dim=in_dim, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
-                 inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
-                 nms_radius=hp["nms_radius"])
-    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
-    m = m.to(gpu_device).eval()
-    f64, c64 = encoder_fp64(g, sd, gpu_device)
-    mx = np.abs(f64).max()
-    e_f = e_c = 0.0
-    for s in range(FP32_REALISATIONS):
-        f32, c32 = encoder_torch(g, sd, gpu_device, torch.float32, seed=s)
-        e_f = max(e_f, np.abs(f32 - f64).max() / mx)
-        e_c = max(e_c, np.abs(c32 - c64).max())
+    g = load_golden(name)
+    assert int(g["in_dim"]) == g["corr_pos"].shape[1]
+    m = _model(g, gpu_device)
+    e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
     rep = lambda a: _t(np.repeat(a[None], B, 0), gpu_device)
     corr, src, tgt = rep(g["corr_pos"]), rep(g["src_keypts"]), rep(g["tgt_keypts"])
     M = kernels.compat(src, tgt, m.sigma_spat)
@@ -149,6 +134,42 @@ def test_wide_layer0_inputs(in_dim, B, gpu_device):
         ours_c = np.abs(conf[b].double().cpu().numpy() - c64).max()
         assert ours_f <= ENVELOPE * e_f + FEAT_FLOOR, (b, ours_f, e_f)
         assert ours_c <= ENVELOPE * e_c + LOGIT_FLOOR, (b, ours_c, e_c)
+    # the whole testing forward against the reference's outputs
+    T, L = m.forward_batched(corr, src, tgt)
+    for b in (0, B - 1):
+        assert np.array_equal(L[b].cpu().numpy(), g["final_labels"]), b
+        np.testing.assert_allclose(T[b].cpu().numpy(), g["final_trans"], atol=POSE_ATOL)
+
+
+@pytest.mark.parametrize("name", ["degen_1k", "rel_1k", "rel_1k_kitti"])
+def test_long_key_chain_encoder(name, gpu_device):
+    """40 copies of a 1000-point golden: the batched plan's attention runs every
+    query's 32 key tiles as ONE online-softmax chain (fused, one split), where a
+    single pair gets many short splits.  Same bars as test_encoder_and_classifier
+    (max and bulk).  r03's V-tile scale (max|v'| up to 2^14) failed this at up to
+    5x the fp32 envelope: the p of keys far below the row max fell under fp16's
+    2^-24 (attention_h3.hpp, h3_vexp)."""
+    import ctypes
+    from pointdsc_amd import _lib, kernels
+    B = 40
+    g = load_golden(name)
+    N = len(g["corr_pos"])
+    fused, npad, nsplit = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(B, N, 0, ctypes.byref(fused)), "encoder_plan")
+    _lib.check(_lib.load().pdsc_attention_layout(B, N, 0, ctypes.byref(npad), ctypes.byref(nsplit)), "layout")
+    assert fused.value == 1 and nsplit.value == 1
+    m = _model(g, gpu_device)
+    rep = lambda a: _t(np.repeat(a[None], B, 0), gpu_device)
+    corr, src, tgt = rep(g["corr_pos"]), rep(g["src_keypts"]), rep(g["tgt_keypts"])
+    feat, _, conf = kernels.encoder(m.pdsc_config(), m.packed_weights(), corr, M=kernels.compat(src, tgt, m.sigma_spat))
+    r_f, r_c = _bulk(name, g, gpu_device)
+    e_f, e_c, f64, c64, mx = _envelope(name, g, gpu_device)
+    for b in (0, B - 1):
+        f, c = feat[b].double().cpu().numpy(), conf[b].double().cpu().numpy()
+        assert np.abs(f - f64).max() / mx <= ENVELOPE * e_f + FEAT_FLOOR, (b, np.abs(f - f64).max() / mx, e_f)
+        assert np.abs(c - c64).max() <= ENVELOPE * e_c + LOGIT_FLOOR, (b, np.abs(c - c64).max(), e_c)
+        assert rms(f - f64) / mx <= BULK * r_f + RMS_FLOOR, (b, rms(f - f64) / mx, r_f)
+        assert rms(c - c64) <= BULK * r_c + RMS_FLOOR, (b, rms(c - c64), r_c)
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -462,14 +483,16 @@ def test_attention_vs_torch_fp64(precision, gpu_device):
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("sv", [1e-3, 1.0, 1e2])
 @pytest.mark.parametrize("sqk", [(1e-3, 1e-3), (7.0, 1.0), (1e2, 1e-1)])
-def test_attention_adversarial_magnitudes(sqk, sv, precision, gpu_device):
+@pytest.mark.parametrize("B,N", [(2, 700), (48, 1024)])  # many short key splits; one 32-tile chain per query
+def test_attention_adversarial_magnitudes(B, N, sqk, sv, precision, gpu_device):
     """Operand magnitudes far from the encoder's O(1): Q, K scaled so the logits are
     ~1e-6 or spread over ~+-20 (softmax weights over > 2^50, i.e. > 30 log2
     units), V scaled by 1e-3 .. 1e2.  Error bound relative to max|V| (the output's
-    scale); the 3xfp16 path keeps small V exact through its per-tile exponent."""
+    scale); the 3xfp16 path keeps small V exact through its per-tile exponent.
+    48 x 1024: the standalone plan runs one key split (a 1024-key online softmax
+    per query), where weights far below the running max must not fall off fp16."""
     from pointdsc_amd import kernels
     torch.manual_seed(1)
-    B, N = 2, 700
     sq, sk = sqk
     q = torch.randn(B, N, 128, device=gpu_device) * sq
     k = torch.randn(B, N, 128, device=gpu_device) * sk
@@ -577,10 +600,12 @@ def test_compat_bit_exact_random_scales(scale, sigma, gpu_device):
     sd = torch.tensor([sigma], dtype=torch.float32, device=gpu_device)
     M = kernels.compat(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
     Mp = kernels.compat_packed(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
+    Mf = kernels.compat_frag(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
     for b in range(B):
         ref = O.compat(src[b], tgt[b], float(np.float32(sigma)))
         assert np.array_equal(M[b], ref), b
         assert np.array_equal(Mp[b], ref), b
+        assert np.array_equal(Mf[b], ref), b
 
 
 @pytest.mark.parametrize("radius", [0.05, 0.1, 0.6])

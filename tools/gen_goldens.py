@@ -61,6 +61,48 @@ def _degenerate(pair):
 
 
 MUTATE = {"degen_1k": _degenerate}
+
+# layer-0 inputs wider than corr_pos (datasets/ThreeDMatch.py:303-315): name -> in_dim.
+# 9: [src, tgt, src - tgt] (src, tgt centred here); 70: centred [src, tgt] + both 32-d
+# descriptors (FCGF's width: 6 + 2 x 32).  The descriptors are synthetic FCGF-like
+# unit vectors; an inlier's target descriptor is its source descriptor plus noise,
+# renormalised, an outlier's an independent draw.  layer0: the trained [128, 6]
+# columns for corr_pos, seeded random columns for the rest.
+WIDE = {"wide9_1k": 9, "wide70_1k": 70}
+CASES["wide9_1k"] = (12, 1000, "3dmatch", 33, 0.3, False, False)
+CASES["wide70_1k"] = (12, 1000, "3dmatch", 32, 0.3, False, False)
+
+
+def _unit_rows(x):
+    return x / np.linalg.norm(x, axis=1, keepdims=True)
+
+
+def wide_inputs(pair, in_dim, seed):
+    """The reference's layer-0 input for in_dim 9 / 70 (ThreeDMatch.py:308-315)."""
+    src, tgt = pair["src_keypts"], pair["tgt_keypts"]
+    if in_dim == 9:  # (src, tgt centred as the 6 / 70 branches do: the trained columns' distribution)
+        c = np.concatenate([src, tgt], axis=-1)
+        return np.concatenate([c - c.mean(0), src - tgt], axis=-1).astype(np.float32), {}
+    rng = np.random.RandomState(seed + 1000)
+    n = src.shape[0]
+    sdesc = _unit_rows(rng.randn(n, 32))
+    tdesc = _unit_rows(rng.randn(n, 32))
+    inl = pair["gt_labels"] > 0
+    tdesc[inl] = _unit_rows(sdesc[inl] + rng.normal(0.0, 0.1, size=sdesc[inl].shape))
+    sdesc, tdesc = sdesc.astype(np.float32), tdesc.astype(np.float32)
+    corr_pos = np.concatenate([src, tgt], axis=-1)
+    corr_pos = corr_pos - corr_pos.mean(0)
+    return np.concatenate([corr_pos, sdesc, tdesc], axis=-1).astype(np.float32), dict(src_desc=sdesc, tgt_desc=tdesc)
+
+
+def wide_layer0(sd_np, in_dim, seed):
+    """layer0 [128, in_dim, 1]: the trained corr_pos columns, seeded random others."""
+    rng = np.random.RandomState(seed + 2000)
+    w6 = sd_np["encoder.layer0.weight"]
+    extra = rng.randn(w6.shape[0], in_dim - 6, 1) / np.sqrt(in_dim)
+    if in_dim == 9:  # src - tgt is metres-scale for outliers: keep the trained columns dominant
+        extra = extra * 0.1
+    return np.concatenate([w6, extra.astype(np.float32)], axis=1).astype(np.float32)
 STORE_FEATURES_MAX_N = 5000  # larger cases keep the logits, not the [N, 128] features
 
 
@@ -84,9 +126,16 @@ def run_case(name):
     pair = synthetic_pair(N, pseed, preset, ratio)
     if name in MUTATE:
         pair = MUTATE[name](pair)
+    in_dim, extra_out = WIDE.get(name, 6), {}
+    if in_dim != 6:
+        wide_corr, extra_out = wide_inputs(pair, in_dim, pseed)
+        pair = dict(pair, corr_pos=wide_corr)
     sd_np = trained_state_dict(preset, L)
+    if in_dim != 6:
+        l0w = wide_layer0(sd_np, in_dim, pseed)
+        sd_np["encoder.layer0.weight"] = l0w
     # ctor exactly as evaluation/test_3DMatch.py:215-224 / test_KITTI.py:280-290
-    model = refmod.PointDSC(in_dim=6, num_layers=L, num_channels=C, num_iterations=10,
+    model = refmod.PointDSC(in_dim=in_dim, num_layers=L, num_channels=C, num_iterations=10,
                             ratio=0.1, inlier_threshold=p["inlier_threshold"],
                             sigma_d=p["sigma_d"], k=40, nms_radius=p["nms_radius"])
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
@@ -102,6 +151,9 @@ def run_case(name):
     scale = float(2.0 ** -m)
     shift = float(np.ceil(max(0.0, 1.0 - lo * scale)))
     sd_np = trained_state_dict(preset, L, shift, scale)
+    if in_dim != 6:
+        sd_np["encoder.layer0.weight"] = l0w
+        extra_out["layer0_weight"] = l0w
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd_np.items()}, strict=True)
 
     rec = {"rigid_calls": []}
@@ -175,6 +227,7 @@ def run_case(name):
         refine_trans=np.stack([t[0].numpy() for t in rec["rigid_calls"][1:]])
         if len(rec["rigid_calls"]) > 1 else np.zeros((0, 4, 4), np.float32),
         M_row_sums=M[0].double().sum(-1).numpy(), M_diag=torch.diagonal(M[0]).numpy(),
+        in_dim=in_dim, **extra_out,
     )
     if store_M:
         out["M"] = M[0].numpy()
