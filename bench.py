@@ -339,6 +339,10 @@ def main():
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
     value = world * P * N * args.steps / elapsed
+    # the fp16 range guard's marks of the last timed step (include/pdsc.h; after the clock)
+    range_marked = len(plan.range_flags())
+    if range_marked:
+        log(f"[rank {rank}] WARNING: {range_marked} pairs marked by the fp16 range guard")
     log(f"[rank {rank}] {ms_per_step:.3f} ms/step -> {value:.4g} correspondences/s")
 
     # the last step's per-pair result rows (libs/loss.py metrics, evaluate.pair_stats), gathered
@@ -607,6 +611,7 @@ def main():
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
+            "range_marked_pairs": range_marked,
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_hbm_dense": roofline_hbm_dense,
             "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,

@@ -39,6 +39,7 @@ enum pdsc_status {
     PDSC_ERR_ARG = 1,         /* bad shape / null pointer / unsupported hyper-parameter */
     PDSC_ERR_HIP = 2,         /* a HIP runtime call failed (launch error) */
     PDSC_ERR_UNSUPPORTED = 3, /* valid for the reference, not implemented here */
+    PDSC_ERR_RANGE = 4,       /* pdsc_range_status: a pair left the fp16 range (below) */
 };
 
 /* Arithmetic of the fp32 contractions (the reference computes them in fp32).
@@ -56,6 +57,24 @@ enum pdsc_precision {
     PDSC_PRECISION_H3 = 0,
     PDSC_PRECISION_F32 = 1,
 };
+
+/* fp16 range guard (PDSC_PRECISION_H3).  The 3xfp16 split is exact only for
+ * |x| < 65520: a larger (or non-finite) activation entering a contraction --
+ * features, Q / K / V, hidden layers; the encoder's are O(10) for the trained
+ * networks -- becomes hi = inf, lo = -inf, and the contraction's output NaN.
+ * The encoder's ReLUs propagate NaN (as torch.relu does), so such a pair ends
+ * with a non-finite logit; the testing and training forwards then (on the
+ * device, asynchronously) mark it in the workspace, set its final_trans to NaN
+ * and its final_labels to 0, and skip its post-refinement: never a silent
+ * finite result.  After the stream has run the forward, pdsc_range_status
+ * reports the marks: PDSC_ERR_RANGE when any pair is marked (flags [B], HOST
+ * int32, may be NULL: 1 for a marked pair), else PDSC_OK.  It synchronises
+ * `stream` and must be given the forward's workspace and B.  Rerun the marked
+ * pairs with PDSC_PRECISION_F32 (pointdsc_amd.PointDSC does that itself).  In
+ * PDSC_PRECISION_F32 a mark means a non-finite logit (non-finite inputs), as
+ * the reference's fp32 would produce.  pdsc_encoder_f32 has no workspace
+ * marks: its conf output carries the NaN.                                    */
+int32_t pdsc_range_status(const void *forward_workspace, int32_t B, int32_t *flags, pdsc_stream_t stream);
 
 /* Hyper-parameters of PointDSC.__init__ (models/PointDSC.py:81-100). */
 typedef struct pdsc_config {
@@ -388,8 +407,9 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
  * kernel arguments, no copy on the stream), each with min(cfg->k, count - 1)
  * = min(cfg->k, N - 1) (every pair keeps the batch's k) and int(count *
  * ratio) >= 1.  debug: as pdsc_forward_testing_debug (may be NULL), with the
- * batch's strides S = int(N * ratio) and k; entries past a pair's own seeds are
- * unspecified.  Workspace: pdsc_forward_workspace_bytes(cfg, B, N).           */
+ * batch's strides S = int(N * ratio) and k; conf rows past counts[b], and seeds,
+ * knn and weights entries past a pair's own seeds, are unspecified.
+ * Workspace: pdsc_forward_workspace_bytes(cfg, B, N).                        */
 int32_t pdsc_forward_testing_ragged(const pdsc_config *cfg, const float *packed, const float *corr_pos,
                                     const float *src, const float *tgt, int32_t B, int32_t N,
                                     const int32_t *counts, float *final_trans, float *final_labels,

@@ -24,6 +24,8 @@ inside the kernels.
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 import torch.nn as nn
 
@@ -71,6 +73,11 @@ class NonLocalNet(nn.Module):
                                   "(or pointdsc_amd.kernels.encoder)")
 
 
+def _rows(tensors, idx):
+    """The batch rows idx of each tensor (idx None: the tensors themselves)."""
+    return tensors if idx is None else tuple(t[idx] for t in tensors)
+
+
 class PointDSC(nn.Module):
     """models/PointDSC.py:80-438 with the testing forward on libpdsc."""
 
@@ -104,25 +111,46 @@ class PointDSC(nn.Module):
             elif isinstance(m, nn.BatchNorm1d):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
-        self._packed = None
-        self._packed_key = None
 
     # ------------------------------------------------------------- internals
-    def pdsc_config(self) -> _lib.PdscConfig:
+    def pdsc_config(self, precision=None) -> _lib.PdscConfig:
         """Hyper-parameters as the C ABI's ``pdsc_config`` (read at call time,
         so attribute edits after construction are honoured like the reference)."""
         return _lib.make_config(self.in_dim, self.num_layers, self.num_channels, self.num_iterations,
-                                self.k, self.ratio, self.inlier_threshold, self.nms_radius, self.precision)
+                                self.k, self.ratio, self.inlier_threshold, self.nms_radius,
+                                precision or self.precision)
 
-    def packed_weights(self) -> torch.Tensor:
-        """Kernel-layout weights, re-packed whenever a parameter/buffer changes."""
+    def packed_weights(self, precision=None) -> torch.Tensor:
+        """Kernel-layout weights, re-packed whenever a parameter/buffer changes
+        (one cached packing per precision)."""
+        precision = precision or self.precision
         named = dict(self.named_parameters())
         named.update(dict(self.named_buffers()))
-        key = (self.precision,) + tuple((n, t.data_ptr(), t._version) for n, t in sorted(named.items()))
-        if self._packed is None or self._packed_key != key:
-            self._packed = kernels.pack_weights(self.pdsc_config(), named)
-            self._packed_key = key
-        return self._packed
+        key = tuple((n, t.data_ptr(), t._version) for n, t in sorted(named.items()))
+        cache = self.__dict__.setdefault("_packed_by_precision", {})
+        if precision not in cache or cache[precision][0] != key:
+            cache[precision] = (key, kernels.pack_weights(self.pdsc_config(precision), named))
+        return cache[precision][1]
+
+    def _range_guarded(self, run):
+        """run(cfg, packed, idx) -> the outputs' tuple for the pairs idx (None: all).
+        Pairs the fp16 range guard marks (kernels.RangeError; include/pdsc.h) are
+        run again with exact fp32 contractions and spliced into the result, so a
+        forward never returns their NaN pose; in 'f32' the error propagates (its
+        marks are non-finite logits, e.g. from non-finite inputs)."""
+        try:
+            return run(self.pdsc_config(), self.packed_weights(), None)
+        except kernels.RangeError as e:
+            if self.precision == "f32":
+                raise
+            warnings.warn(f"pairs {e.pairs}: activations beyond fp16's range in the 3xfp16 path; "
+                          f"recomputed with exact fp32 contractions", RuntimeWarning, stacklevel=3)
+            out, redo = e.outputs, run(self.pdsc_config("f32"), self.packed_weights("f32"), e.pairs)
+            idx = torch.tensor(e.pairs, device=out[0].device)
+            for t, r in zip(out, redo):
+                if t is not None:
+                    t[idx] = r
+            return out
 
     # --------------------------------------------------------------- forward
     def forward(self, data):
@@ -135,11 +163,12 @@ class PointDSC(nn.Module):
                 raise NotImplementedError(
                     "training-mode forward in model.train() (BatchNorm batch statistics, autograd) is out of "
                     "scope for the MI355X build; call model.eval() for the validation forward (DESIGN.md)")
-            trans, conf, M, _ = kernels.forward_training(self.pdsc_config(), self.packed_weights(), corr_pos, src,
-                                                         tgt)
+            trans, conf, M, _ = self._range_guarded(lambda cfg, pk, i: kernels.forward_training(
+                cfg, pk, *_rows((corr_pos, src, tgt), i)))
             return {"final_trans": trans, "final_labels": conf, "M": M}
         assert corr_pos.shape[0] == 1  # pick_seeds / post_refinement support bs = 1 only
-        trans, labels = kernels.forward_testing(self.pdsc_config(), self.packed_weights(), corr_pos, src, tgt)
+        trans, labels = self._range_guarded(lambda cfg, pk, i: kernels.forward_testing(
+            cfg, pk, *_rows((corr_pos, src, tgt), i)))
         return {"final_trans": trans, "final_labels": labels, "M": None}
 
     def forward_list(self, datas):
@@ -155,12 +184,37 @@ class PointDSC(nn.Module):
         corr, counts = kernels.pad_pairs([d["corr_pos"] for d in datas])
         src, _ = kernels.pad_pairs([d["src_keypts"] for d in datas])
         tgt, _ = kernels.pad_pairs([d["tgt_keypts"] for d in datas])
-        trans, labels = kernels.forward_ragged(self.pdsc_config(), self.packed_weights(), corr, src, tgt, counts)
+        trans, labels = self.forward_padded(corr, src, tgt, counts)
         return [{"final_trans": trans[b:b + 1], "final_labels": labels[b:b + 1, :n], "M": None}
                 for b, n in enumerate(counts)]
+
+    def forward_padded(self, corr_pos, src_keypts, tgt_keypts, counts):
+        """A zero-padded ragged batch (kernels.pad_pairs): pair b in the first
+        counts[b] rows.  Returns (final_trans [B,4,4], final_labels [B,N], rows past
+        counts[b] 0), each pair as its own bs = 1 ``forward``.  The ragged kernels
+        run every pair with the batch's neighbourhood k (include/pdsc.h); a pair
+        with count <= k, whose forward clips k to count - 1 (:250), runs alone."""
+        counts = [int(c) for c in counts]
+        B, N = corr_pos.shape[:2]
+        big = [b for b, n in enumerate(counts) if n >= self.k + 1]
+        if len(big) == B:
+            return self._range_guarded(lambda cfg, pk, i: kernels.forward_ragged(
+                cfg, pk, *_rows((corr_pos, src_keypts, tgt_keypts), i),
+                counts if i is None else [counts[b] for b in i]))
+        trans = torch.empty((B, 4, 4), dtype=torch.float32, device=corr_pos.device)
+        labels = torch.zeros((B, N), dtype=torch.float32, device=corr_pos.device)
+        if big:
+            T, L = self.forward_padded(*_rows((corr_pos, src_keypts, tgt_keypts), big), [counts[b] for b in big])
+            trans[big], labels[big] = T, L
+        for b in (b for b in range(B) if counts[b] < self.k + 1):
+            n = counts[b]
+            r = self({"corr_pos": corr_pos[b:b + 1, :n], "src_keypts": src_keypts[b:b + 1, :n],
+                      "tgt_keypts": tgt_keypts[b:b + 1, :n], "testing": True})
+            trans[b], labels[b, :n] = r["final_trans"][0], r["final_labels"][0]
+        return trans, labels
 
     def forward_batched(self, corr_pos, src_keypts, tgt_keypts):
         """B independent pairs in one call (same N): (final_trans [B,4,4], final_labels [B,N]).
         Equivalent to B calls of ``forward`` with bs = 1."""
-        return kernels.forward_testing(self.pdsc_config(), self.packed_weights(), corr_pos, src_keypts,
-                                       tgt_keypts)
+        return self._range_guarded(lambda cfg, pk, i: kernels.forward_testing(
+            cfg, pk, *_rows((corr_pos, src_keypts, tgt_keypts), i)))

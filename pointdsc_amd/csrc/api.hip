@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "pdsc_internal.hpp"
 
@@ -251,6 +252,7 @@ static bool ragged_order_on() {
 }
 
 struct FwdBufs {
+    int *range;  // [B] the fp16 range guard's per-pair flags: the workspace's first bytes (pdsc_range_status)
     float *M, *normed, *conf, *lm, *kdist, *seed_trans, *weights, *hsums;
     _Float16 *normed_s;
     int *seeds, *knn, *counts;
@@ -261,6 +263,7 @@ struct FwdBufs {
 
 FwdBufs carve_forward(Carve &c, const Dims &d) {
     FwdBufs f;
+    f.range = c.take<int>((size_t)d.B);  // first: at the workspace's base
     // symmetric-packed tiles (PDSC_DENSE_M=1: the dense [N][N] form, for A/B measurement)
     f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), mfrag_floats(d.N)));  // (mfrag >= N^2: dense fits)
     f.enc = carve_encoder(c, d);
@@ -740,12 +743,12 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
                              f.seed_trans, f.counts, f.hsums, s, rg));
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
-                              nullptr, nullptr, final_trans, final_labels, s, rg));
+                              nullptr, nullptr, final_trans, final_labels, s, rg, f.conf, f.range));
     if (dbg->trans_pre_refine)
         HIPCHK(hipMemcpyAsync(dbg->trans_pre_refine, final_trans, sizeof(float) * 16 * d.B, hipMemcpyDeviceToDevice, s));
     STAGE(6);
     // a11 (:186, :403-438)
-    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s, rg));
+    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s, rg, f.range));
     STAGE(7);
 #undef STAGE
     if (dbg->conf) HIPCHK(hipMemcpyAsync(dbg->conf, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
@@ -819,9 +822,24 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
                              f.counts, f.hsums, s));
     // the labels of the best hypothesis are not returned in training mode (:189-191): f.lm is scratch
     HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold, nullptr,
-                              nullptr, final_trans, f.lm, s));
+                              nullptr, final_trans, f.lm, s, {}, f.conf, f.range));
     HIPCHK(hipMemcpyAsync(confidence, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));
     if (seeds_out) HIPCHK(hipMemcpyAsync(seeds_out, f.seeds, sizeof(int) * d.B * d.S, hipMemcpyDeviceToDevice, s));
+    return PDSC_OK;
+}
+
+int32_t pdsc_range_status(const void *ws, int32_t B, int32_t *flags, pdsc_stream_t stream) {
+    if (!ws || B < 1) return fail(PDSC_ERR_ARG, "ws=%p B=%d", ws, B);
+    std::vector<int32_t> h((size_t)B);
+    hipStream_t s = S_(stream);
+    HIPCHK(hipMemcpyAsync(h.data(), ws, sizeof(int32_t) * B, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int bad = 0;
+    for (int b = 0; b < B; ++b) {
+        if (flags) flags[b] = h[b];
+        bad += h[b] != 0;
+    }
+    if (bad) return fail(PDSC_ERR_RANGE, "%d of %d pairs left the fp16 range (rerun them with PDSC_PRECISION_F32)", bad, B);
     return PDSC_OK;
 }
 

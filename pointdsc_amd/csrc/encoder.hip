@@ -384,6 +384,14 @@ hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int N
 // (row tile, column tile) per wave so all four waves stay busy.
 enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
 
+// ReLU that keeps NaN (torch.relu(nan) = nan; fmaxf(nan, 0) = 0).  The fp16
+// range guard relies on it: a 3xfp16 operand beyond fp16's range (hi = inf,
+// lo = -inf) makes its contraction NaN, and this carries the NaN on to the
+// logits, where select_best_kernel flags the pair (pdsc.h, PDSC_ERR_RANGE)
+// instead of a ReLU silently zeroing it.  Same value as fmaxf(x, 0) for every
+// non-NaN x (-0 -> +0).  IEEE 754-2019 maximum: one v_maximum3_f32 on gfx950.
+PDSC_DEV float relu_nan(float x) { return __builtin_elementwise_maximum(x, 0.0f); }
+
 constexpr int S132 = CH + 4, S68 = CH2 + 4, S36 = CLS + 4;
 constexpr int IN_MAX = 16;     // layer0 input width held in registers (pw_first)
 constexpr int IN_LIMIT = 128;  // layer0 input width supported (datasets/ThreeDMatch.py:311-315: 70)
@@ -474,8 +482,8 @@ PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, 
         for (int r = 0; r < 16; ++r) {
             const int row = (rt0 + i) * 32 + acc_row(r, h);
             float y = acc[i][r] * inv + bias;
-            if (EPI == EPI_BN_RELU) y = fmaxf(y * al + be, 0.0f);  // eval BN as torch folds it, ReLU
-            if (EPI == EPI_RELU) y = fmaxf(y, 0.0f);
+            if (EPI == EPI_BN_RELU) y = relu_nan(y * al + be);  // eval BN as torch folds it, ReLU
+            if (EPI == EPI_RELU) y = relu_nan(y);
             if (EPI == EPI_RESID) y = resid[row * CH + j] + y;      // res = feat + message (:44)
             Y[row * ystr + j] = y;
         }
@@ -1099,8 +1107,8 @@ PDSC_DEV void w2_epilogue(f32x16 (&acc)[OUT / 32], float inv, const float *cf, c
             for (int e = 0; e < 8; ++e) {
                 const int r = 8 * u + e;
                 float y = __builtin_fmaf(acc[t][r], inv, e < 4 ? b0[e] : b1[e - 4]);  // exact acc 2^-s, one rounding
-                if (EPI == EPI_BN_RELU) y = fmaxf(y * (e < 4 ? a0[e] : a1[e - 4]) + (e < 4 ? e0[e] : e1[e - 4]), 0.0f);
-                if (EPI == EPI_RELU) y = fmaxf(y, 0.0f);
+                if (EPI == EPI_BN_RELU) y = relu_nan(y * (e < 4 ? a0[e] : a1[e - 4]) + (e < 4 ? e0[e] : e1[e - 4]));
+                if (EPI == EPI_RELU) y = relu_nan(y);
                 if (EPI == EPI_RESID) y = resid[t][r] + y;  // res = feat + message (:44)
                 acc[t][r] = y;
                 v[e] = y;

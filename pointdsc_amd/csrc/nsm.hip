@@ -981,11 +981,26 @@ __global__ __launch_bounds__(256) void select_best_kernel(const float *__restric
                                                           float tau, float *__restrict__ fitness,
                                                           int *__restrict__ best_out,
                                                           float *__restrict__ trans,
-                                                          float *__restrict__ labels, Ragged rg) {
+                                                          float *__restrict__ labels, Ragged rg,
+                                                          const float *__restrict__ conf, int *__restrict__ range) {
     __shared__ int wbest[4], wcnt[4];
     __shared__ float Ts[16];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);  // this pair's sizes; Nstr, Sstr: the strides
+    if (conf) {
+        // the fp16 range guard (pdsc.h, PDSC_ERR_RANGE): an activation that left
+        // fp16's range in a 3xfp16 contraction turns into NaN (inf hi, -inf lo),
+        // which the encoder's NaN-propagating ReLUs carry into every logit
+        int bad = 0;
+        for (int n = tid; n < N; n += 256) bad |= !__builtin_isfinite(conf[(size_t)b * Nstr + n]);
+        bad = __syncthreads_or(bad);
+        if (range && tid == 0) range[b] = bad;
+        if (bad) {
+            if (tid < 16) trans[(size_t)b * 16 + tid] = __builtin_nanf("");
+            for (int n = tid; n < Nstr; n += 256) labels[(size_t)b * Nstr + n] = 0.0f;
+            return;  // workgroup-uniform
+        }
+    }
     int bc = -1, bi = 0x7fffffff;
     for (int s = tid; s < S; s += 256) {
         const int c = counts[(size_t)b * Sstr + s];
@@ -1027,9 +1042,10 @@ __global__ __launch_bounds__(256) void select_best_kernel(const float *__restric
 
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
                               const int *counts, int B, int N, int S, float tau, float *fitness,
-                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg) {
+                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg, const float *conf,
+                              int *range) {
     hipLaunchKernelGGL(select_best_kernel, dim3(B), dim3(256), 0, s, src, tgt, seed_trans, counts, N, S,
-                       tau, fitness, best, trans, labels, rg);
+                       tau, fitness, best, trans, labels, rg, conf, range);
     return hipGetLastError();
 }
 
@@ -1095,10 +1111,11 @@ PDSC_DEV void block_rigid(const float *__restrict__ A, const float *__restrict__
 __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ trans,
                                                          const float *__restrict__ src,
                                                          const float *__restrict__ tgt, int Nstr,
-                                                         float thr, Ragged rg) {
+                                                         float thr, Ragged rg, const int *__restrict__ range) {
     __shared__ float red[RW][9];
     __shared__ float Ts[16];
     const int b = blockIdx.x, tid = threadIdx.x;
+    if (range && range[b]) return;  // a pair the range guard flagged keeps its NaN pose (workgroup-uniform)
     const int N = rg.n(b, Nstr);  // this pair's correspondences; Nstr: the stride
     const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
     if (tid < 16) Ts[tid] = trans[(size_t)b * 16 + tid];
@@ -1135,8 +1152,8 @@ __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ tra
 }
 
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
-                              hipStream_t s, Ragged rg) {
-    hipLaunchKernelGGL(post_refine_kernel, dim3(B), dim3(RB), 0, s, trans, src, tgt, N, thr, rg);
+                              hipStream_t s, Ragged rg, const int *range) {
+    hipLaunchKernelGGL(post_refine_kernel, dim3(B), dim3(RB), 0, s, trans, src, tgt, N, thr, rg, range);
     return hipGetLastError();
 }
 

@@ -248,11 +248,15 @@ hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int 
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
                              float *sums, hipStream_t s, Ragged rg = {});
+// conf / range (both may be null): the forward's fp16 range guard -- a pair
+// whose logits conf[b, :n] hold a non-finite value gets range[b] = 1 (else 0),
+// final_trans all NaN and labels 0; post_refine leaves such a pair alone.
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
                               const int *counts, int B, int N, int S, float tau, float *fitness,
-                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg = {});
+                              int *best, float *trans, float *labels, hipStream_t s, Ragged rg = {},
+                              const float *conf = nullptr, int *range = nullptr);
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
-                              hipStream_t s, Ragged rg = {});
+                              hipStream_t s, Ragged rg = {}, const int *range = nullptr);
 hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
                         hipStream_t s);
 

@@ -181,7 +181,7 @@ def evaluate_synthetic(model, n_pairs, num_corr, preset="3dmatch", batch=16, see
         t_data = (time.perf_counter() - t0) / len(idx)
         t0 = time.perf_counter()
         if ragged:
-            T, L = kernels.forward_ragged(model.pdsc_config(), model.packed_weights(), corr, src, tgt, counts)
+            T, L = model.forward_padded(corr, src, tgt, counts)
         else:
             T, L = model.forward_batched(corr, src, tgt)
         if device is not None and device.type == "cuda":

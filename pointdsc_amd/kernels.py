@@ -239,6 +239,40 @@ def post_refine(trans, src, tgt, thr: float):
 
 
 # ----------------------------------------------------------------- forward
+PDSC_ERR_RANGE = 4
+
+
+class RangeError(RuntimeError):
+    """PDSC_ERR_RANGE (include/pdsc.h, fp16 range guard): pairs whose activations
+    left fp16's range under PDSC_PRECISION_H3 (or, in either precision, whose
+    logits are non-finite).  ``pairs``: their indices in the call; ``outputs``:
+    the call's return value, valid for every other pair (the marked pairs'
+    final_trans are NaN, their final_labels 0)."""
+
+    def __init__(self, pairs, outputs):
+        super().__init__(f"pairs {pairs} left the fp16 range of the 3xfp16 contractions "
+                         f"(rerun them with precision='f32')")
+        self.pairs, self.outputs = list(pairs), outputs
+
+
+def range_flags(ws, B, device):
+    """The forward's per-pair range marks from its workspace (pdsc_range_status;
+    synchronises the device's current stream): a list of marked pair indices."""
+    L = _lib.load()
+    flags = (ctypes.c_int32 * B)()
+    st = L.pdsc_range_status(_p(ws), B, flags, _stream(device))
+    if st not in (0, PDSC_ERR_RANGE):
+        check(st, "pdsc_range_status")
+    return [b for b in range(B) if flags[b]]
+
+
+def _range_check(ws, B, device, outputs):
+    bad = range_flags(ws, B, device)
+    if bad:
+        raise RangeError(bad, outputs)
+    return outputs
+
+
 def _check_inputs(cfg, corr_pos, src, tgt):
     """Shapes the forward kernels assume (the reference's Conv1d(in_dim) raises on a wrong width)."""
     if src.dim() != 3 or src.shape[2] != 3 or tgt.shape != src.shape or corr_pos.dim() != 3 \
@@ -247,9 +281,10 @@ def _check_inputs(cfg, corr_pos, src, tgt):
                          f"src {tuple(src.shape)}, tgt {tuple(tgt.shape)} (expected [B,N,3])")
 
 
-def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
+def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False, check_range=True):
     """Full testing forward for B pairs: (final_trans [B,4,4], final_labels [B,N])
-    (+ (confidence [B,N], seeds [B,S]) when ``debug``)."""
+    (+ (confidence [B,N], seeds [B,S]) when ``debug``).  check_range: read the
+    fp16 range guard's marks (synchronises) and raise RangeError if any."""
     corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
     B, N, _ = src.shape
     _check_inputs(cfg, corr_pos, src, tgt)
@@ -268,12 +303,11 @@ def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False):
     check(L.pdsc_forward_testing(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
                                  _p(trans), _p(labels), _p(conf), _p(seeds), _p(ws), nb, _stream(dev)),
           "pdsc_forward_testing")
-    if debug:
-        return trans, labels, conf, seeds
-    return trans, labels
+    out = (trans, labels, conf, seeds) if debug else (trans, labels)
+    return _range_check(ws, B, dev, out) if check_range else out
 
 
-def forward_stages(cfg, packed, corr_pos, src, tgt):
+def forward_stages(cfg, packed, corr_pos, src, tgt, check_range=True):
     """The full testing forward for B pairs with every stage's output
     (pdsc_forward_testing_debug): dict of final_trans [B,4,4], final_labels
     [B,N], conf [B,N], seeds [B,S], knn [B,S,k], weights [B,S,k],
@@ -297,10 +331,10 @@ def forward_stages(cfg, packed, corr_pos, src, tgt):
     check(L.pdsc_forward_testing_debug(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
                                        _p(out["final_trans"]), _p(out["final_labels"]), ctypes.byref(dbg), _p(ws), nb,
                                        _stream(dev)), "pdsc_forward_testing_debug")
-    return out
+    return _range_check(ws, B, dev, out) if check_range else out
 
 
-def forward_ragged(cfg, packed, corr_pos, src, tgt, counts, debug=False):
+def forward_ragged(cfg, packed, corr_pos, src, tgt, counts, debug=False, check_range=True):
     """B pairs of different sizes in one call (pdsc_forward_testing_ragged): pair
     b occupies the first counts[b] rows of the padded [B,N,.] inputs.  Returns
     (final_trans [B,4,4], final_labels [B,N], rows past counts[b] zero); with
@@ -333,7 +367,8 @@ def forward_ragged(cfg, packed, corr_pos, src, tgt, counts, debug=False):
     check(L.pdsc_forward_testing_ragged(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N, cnt,
                                         _p(trans), _p(labels), ctypes.byref(dbg) if dbg is not None else None, _p(ws),
                                         nb, _stream(dev)), "pdsc_forward_testing_ragged")
-    return (trans, labels, st) if debug else (trans, labels)
+    out = (trans, labels, st) if debug else (trans, labels)
+    return _range_check(ws, B, dev, out) if check_range else out
 
 
 def pad_pairs(tensors, N=None):
@@ -348,7 +383,7 @@ def pad_pairs(tensors, N=None):
     return out, counts
 
 
-def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=False):
+def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=False, check_range=True):
     """Training-mode forward (models/PointDSC.py:158-163, :176, :182, :189-191) for
     B pairs: (final_trans [B,4,4], confidence [B,N], M [B,N,N] | None,
     seeds [B,S] | None).  Forward only: no gradients flow through the HIP path."""
@@ -368,7 +403,8 @@ def forward_training(cfg, packed, corr_pos, src, tgt, want_M=True, want_seeds=Fa
     check(L.pdsc_forward_training(ctypes.byref(cfg), _p(packed), _p(corr_pos), _p(src), _p(tgt), B, N,
                                   _p(trans), _p(conf), _p(M), _p(seeds), _p(ws), nb, _stream(dev)),
           "pdsc_forward_training")
-    return trans, conf, M, seeds
+    out = (trans, conf, M, seeds)
+    return _range_check(ws, B, dev, out) if check_range else out
 
 
 def spectral_matching_loss(M, gt_labels, balanced=True):
@@ -413,6 +449,10 @@ class ForwardPlan:
             ctypes.byref(self.cfg), _p(self.packed), _p(corr_pos), _p(src), _p(tgt), self.B, self.N,
             _p(self.trans), _p(self.labels), None, None, _p(self.ws), self.nb, s), "pdsc_forward_testing")
         return self.trans, self.labels
+
+    def range_flags(self):
+        """The last forward's fp16 range marks (pdsc_range_status; synchronises)."""
+        return range_flags(self.ws, self.B, self.ws.device)
 
     def capture(self, corr_pos, src, tgt):
         """Record one forward over these (resident) inputs into a HIP graph;

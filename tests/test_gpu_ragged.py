@@ -123,3 +123,46 @@ def test_ragged_vs_single_forwards(B, gpu_device):
         r = m(dict(ds[b], testing=True))
         assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
         np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
+
+
+@pytest.mark.parametrize("sizes", [[777, 1000, 3000, 2111, 5000],  # key-split plan
+                                   [1000 - 7 * i for i in range(40)],  # fused attention + chain
+                                   [5000 - 13 * i for i in range(8)]])  # 64-query-wave split plan
+def test_ragged_padding_content_ignored(sizes, gpu_device):
+    """Rows past counts[b] are ignored whatever they hold (include/pdsc.h): NaN
+    corr_pos and 1e30 coordinates there give bitwise the zero-padded call's poses,
+    labels and the pairs' own logits -- and no range-guard mark."""
+    from pointdsc_amd import kernels
+    m, _ = _model(gpu_device)
+    ds = _datas(_pairs(sizes, seed=81), gpu_device)
+    N = max(sizes)
+    corr, counts = kernels.pad_pairs([d["corr_pos"] for d in ds], N)
+    src, _ = kernels.pad_pairs([d["src_keypts"] for d in ds], N)
+    tgt, _ = kernels.pad_pairs([d["tgt_keypts"] for d in ds], N)
+    T, L, st = kernels.forward_ragged(m.pdsc_config(), m.packed_weights(), corr, src, tgt, counts, debug=True)
+    c2, s2, t2 = corr.clone(), src.clone(), tgt.clone()
+    for b, n in enumerate(counts):
+        c2[b, n:] = float("nan")
+        s2[b, n:] = 1e30
+        t2[b, n:] = -1e30
+    T2, L2, st2 = kernels.forward_ragged(m.pdsc_config(), m.packed_weights(), c2, s2, t2, counts, debug=True)
+    assert torch.equal(T, T2) and torch.equal(L, L2)
+    for b, n in enumerate(counts):
+        assert torch.equal(st["conf"][b, :n], st2["conf"][b, :n]), b
+
+
+def test_forward_list_small_pairs(gpu_device):
+    """Pairs with count <= k (their forward clips k to count - 1, :250) in a list
+    with larger ones: forward_list runs them alone (bitwise their own forward),
+    the rest as one ragged batch; every pair matches its own forward."""
+    m, _ = _model(gpu_device)
+    sizes = [30, 1000, 41, 800, 12]
+    ds = _datas(_pairs(sizes, seed=82), gpu_device)
+    res = m.forward_list(ds)
+    for b, n in enumerate(sizes):
+        r = m(dict(ds[b], testing=True))
+        assert res[b]["final_labels"].shape == (1, n)
+        assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
+        if n <= 40:
+            assert torch.equal(r["final_trans"], res[b]["final_trans"]), b
+        np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)

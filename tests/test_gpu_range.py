@@ -1,0 +1,116 @@
+"""The fp16 range guard (include/pdsc.h, PDSC_ERR_RANGE; run with -m gpu).
+
+A pair whose coordinates are scaled by 1e5 drives the encoder's activations far
+past fp16's 65504, where the 3xfp16 split cannot represent them.  The bar: no
+call ever hands back that pair's NaN pose as a success --
+  * the testing forward marks it (pdsc_range_status -> PDSC_ERR_RANGE, the
+    kernels wrappers raise RangeError), poisons its pose (NaN) and labels (0),
+    and leaves every other pair of the batch bitwise as without it;
+  * the module (PointDSC.forward_batched / forward / forward_list) reruns the
+    marked pair with exact fp32 contractions: its result is bitwise the 'f32'
+    model's, the other pairs' the 'h3' model's;
+  * the exact-fp32 mode itself takes the scaled pair without a mark;
+  * a normal batch has no marks (PDSC_OK)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SCALE = 1e5
+
+
+def _model(dev, precision):
+    from pointdsc_amd.PointDSC import PointDSC
+    from pointdsc_amd.synthetic import BENCH_CLS, PRESETS, trained_state_dict
+    p = PRESETS["3dmatch"]
+    m = PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40, nms_radius=p["nms_radius"],
+                 precision=precision)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict("3dmatch", 12, *BENCH_CLS).items()})
+    return m.to(dev).eval()
+
+
+def _batch(dev, B=4, N=1000, bad=(2,)):
+    from pointdsc_amd.synthetic import synthetic_pair
+    ps = [synthetic_pair(N, 4242 + i) for i in range(B)]
+    corr = np.stack([q["corr_pos"] for q in ps])
+    for b in bad:
+        corr[b] = corr[b] * SCALE
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t(corr), t(np.stack([q["src_keypts"] for q in ps])), t(np.stack([q["tgt_keypts"] for q in ps]))
+
+
+def test_range_marks_and_poisons(gpu_device):
+    from pointdsc_amd import kernels
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device)
+    with pytest.raises(kernels.RangeError) as ei:
+        kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr, src, tgt)
+    assert ei.value.pairs == [2]
+    T, L = ei.value.outputs
+    assert torch.isnan(T[2]).all() and float(L[2].abs().sum()) == 0.0
+    # the other pairs: bitwise as in the same batch without the scaled pair
+    corr0, _, _ = _batch(gpu_device, bad=())
+    T0, L0 = kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr0, src, tgt)
+    for b in (0, 1, 3):
+        assert torch.equal(T[b], T0[b]) and torch.equal(L[b], L0[b]), b
+        assert torch.isfinite(T[b]).all()
+    # the C ABI: PDSC_ERR_RANGE with the flags; PDSC_OK on the normal batch
+    from pointdsc_amd import _lib
+    L_ = _lib.load()
+    plan = kernels.ForwardPlan(m.pdsc_config(), m.packed_weights(), 4, 1000, gpu_device)
+    plan.run(corr, src, tgt)
+    flags = (ctypes.c_int32 * 4)()
+    assert L_.pdsc_range_status(kernels._p(plan.ws), 4, flags, kernels._stream(gpu_device)) == kernels.PDSC_ERR_RANGE
+    assert list(flags) == [0, 0, 1, 0]
+    plan.run(corr0, src, tgt)
+    assert L_.pdsc_range_status(kernels._p(plan.ws), 4, flags, kernels._stream(gpu_device)) == 0
+    assert list(flags) == [0, 0, 0, 0]
+
+
+def test_module_reruns_marked_pairs_in_f32(gpu_device):
+    m, m32 = _model(gpu_device, "h3"), _model(gpu_device, "f32")
+    corr, src, tgt = _batch(gpu_device)
+    with pytest.warns(RuntimeWarning, match="fp16"):
+        T, L = m.forward_batched(corr, src, tgt)
+    assert torch.isfinite(T).all()
+    # the scaled pair: the exact-fp32 model's result on it alone; the rest: the h3 batch's
+    T32, L32 = m32.forward_batched(corr[2:3], src[2:3], tgt[2:3])
+    assert torch.equal(T[2], T32[0]) and torch.equal(L[2], L32[0])
+    corr0, _, _ = _batch(gpu_device, bad=())
+    T0, L0 = m.forward_batched(corr0, src, tgt)
+    for b in (0, 1, 3):
+        assert torch.equal(T[b], T0[b]) and torch.equal(L[b], L0[b])
+    # bs = 1 forward and the ragged list take the same route
+    with pytest.warns(RuntimeWarning):
+        r = m({"corr_pos": corr[2:3], "src_keypts": src[2:3], "tgt_keypts": tgt[2:3], "testing": True})
+    assert torch.equal(r["final_trans"], T32) and torch.equal(r["final_labels"], L32)
+    ds = [{"corr_pos": corr[b:b + 1, :n], "src_keypts": src[b:b + 1, :n], "tgt_keypts": tgt[b:b + 1, :n]}
+          for b, n in zip(range(4), (1000, 900, 950, 1000))]
+    with pytest.warns(RuntimeWarning):
+        res = m.forward_list(ds)
+    assert all(torch.isfinite(x["final_trans"]).all() for x in res)
+
+
+def test_f32_mode_takes_the_scaled_pair(gpu_device):
+    from pointdsc_amd import kernels
+    m32 = _model(gpu_device, "f32")
+    corr, src, tgt = _batch(gpu_device)
+    T, L = kernels.forward_testing(m32.pdsc_config(), m32.packed_weights(), corr, src, tgt)  # no RangeError
+    assert torch.isfinite(T).all()
+
+
+def test_training_forward_range_guard(gpu_device):
+    from pointdsc_amd import kernels
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device)
+    with pytest.raises(kernels.RangeError) as ei:
+        kernels.forward_training(m.pdsc_config(), m.packed_weights(), corr, src, tgt, want_M=False)
+    assert ei.value.pairs == [2]
+    assert torch.isnan(ei.value.outputs[0][2]).all()
+    with pytest.warns(RuntimeWarning):
+        r = m({"corr_pos": corr, "src_keypts": src, "tgt_keypts": tgt})
+    assert torch.isfinite(r["final_trans"]).all()
