@@ -715,7 +715,9 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
 #define STAGE(i) \
     if (ev) HIPCHK(hipEventRecord(ev[i], s))
     STAGE(0);
-    // a1 (:150-153)
+    // a1 (:150-153).  (r04: a1 on a second stream beside the encoder's first
+    // launch measured no gain at 128 x 1000 / 8 x 5000 and +44 us per single
+    // pair -- the cross-stream event pair -- so the forward stays on one stream.)
     const int mlay = forward_m_layout(d);
     if (mlay == M_FRAG)
         HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));

@@ -186,21 +186,21 @@ PDSC_DEV f32x16 mfma_h3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x16 c) {
     return mfma_h(ah, bh, c);
 }
 
-// Products with a three-plane weight w = wh + wm + wl (every fp32 weight
-// exactly, encoder.hip: pack_dense_kernel) and a two-plane activation x = xh + xl:
-// x.w ~= xh.(wh + wm + wl) + xl.wh, small terms first.  The dropped xl.(wm + wl)
-// is 2^-22 relative and data-dependent; the weights themselves carry no
-// representation error (a 2-plane weight's 2^-23 error is the same perturbation
-// of the model for every point and measurably dominates the encoder's error).
+// Products with a W_PLANES-plane weight w = wh + wm (+ wl) (encoder.hip:
+// pack_dense_kernel) and a two-plane activation x = xh + xl:
+// x.w ~= xh.(wh + wm (+ wl)) + xl.wh, small terms first.  The dropped xl.wm is
+// 2^-22 relative, as is a 2-plane weight's representation error (r01-r03 kept
+// the lo plane: every fp32 weight exactly, one more product; r04 measured the
+// two forms inside the same fp32 noise, tools/emulate_conv.py).
 // mfma_xw3: A = activations (rows = points), B = weights; mfma_w3x: transposed.
 PDSC_DEV f32x16 mfma_xw3(f16x8 xh, f16x8 xl, f16x8 wh, f16x8 wm, f16x8 wl, f32x16 c) {
-    c = mfma_h(xh, wl, c);
+    if constexpr (W_PLANES == 3) c = mfma_h(xh, wl, c);
     c = mfma_h(xh, wm, c);
     c = mfma_h(xl, wh, c);
     return mfma_h(xh, wh, c);
 }
 PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x16 c) {
-    c = mfma_h(wl, xh, c);
+    if constexpr (W_PLANES == 3) c = mfma_h(wl, xh, c);
     c = mfma_h(wm, xh, c);
     c = mfma_h(wh, xl, c);
     return mfma_h(wh, xh, c);

@@ -269,11 +269,20 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     const float *ev_lds = reinterpret_cast<const float *>(smem + W64_RING);
     auto load_ev = [&](int st) { return ev_lds[st]; };  // (wave-uniform address: one broadcast read)
 
+#ifdef W64_EXP_NO_LDSREAD  // diagnostic: fragments read once, then reused (no ds_read in the loop)
+    bool lds_once = true;
+#endif
     auto kread = [&](const char *Kl, int j, f16x8(&f)[2]) {
+#ifdef W64_EXP_NO_LDSREAD
+        if (!lds_once) return;
+#endif
         f[0] = *reinterpret_cast<const f16x8 *>(Kl + 2 * h3_frag(j, 0, lane));
         f[1] = *reinterpret_cast<const f16x8 *>(Kl + 2 * h3_frag(j, 1, lane));
     };
     auto vread = [&](const char *Vl, int i, f16x8(&f)[2]) {  // fragment i = (t, s) = (i / 2, i % 2)
+#ifdef W64_EXP_NO_LDSREAD
+        if (!lds_once) return;
+#endif
         f[0] = *reinterpret_cast<const f16x8 *>(Vl + 2 * h3_frag(i, 0, lane));
         f[1] = *reinterpret_cast<const f16x8 *>(Vl + 2 * h3_frag(i, 1, lane));
     };
@@ -289,6 +298,11 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     // arithmetic, not the first tile)
     auto sm1_slice = [&](auto kc, int u, const f32x16 &S, const f32x4 (&mv)[4], float ev, int key0, SmA &a) {
         constexpr int k = decltype(kc)::value;
+#ifdef W64_EXP_NO_SM1  // diagnostic: no part-1 VALU (p = S)
+        if constexpr (k >= 1 && k <= 16) a.p[k - 1] = S[k - 1];
+        if constexpr (k == 22) a.resc = false;
+        return;
+#endif
         if constexpr (k == 0) {
             a.mb0 = m_run[u] - (float)H3_PSHIFT + ev;
             a.mx = -INFINITY;
@@ -364,6 +378,14 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     };
     auto sm2_slice = [&](auto kc, int u, const SmA &a, float ev, SmB &w, f16x8(&ph)[2], f16x8(&pl)[2]) {
         constexpr int k = decltype(kc)::value;
+#ifdef W64_EXP_NO_SM2  // diagnostic: no part-2 VALU (P = the bits of p)
+        if constexpr (k < 8) {
+            auto hs = __builtin_bit_cast(u32x4, ph[k >> 2]);
+            hs[k & 3] = __builtin_bit_cast(uint32_t, a.p[2 * k]);
+            ph[k >> 2] = pl[k >> 2] = __builtin_bit_cast(f16x8, hs);
+        }
+        return;
+#endif
         if constexpr (k == 0) w.psum = 0.0f;
         if constexpr (k < 16) {
             w.ex[k] = __builtin_amdgcn_exp2f(a.p[k]);
@@ -576,6 +598,9 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         rebase(std::integral_constant<int, 1>{}, sa[1]);
         W64_ST(si + 5);
     };
+#ifdef W64_EXP_NO_LDSREAD
+    lds_once = false;
+#endif
     int t = st0 + 1;
     for (; t + 1 < st1; t += 2) {
         tile(t, mY, eY, eX, mX, eX);

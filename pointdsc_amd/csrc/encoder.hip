@@ -55,10 +55,10 @@ __global__ __launch_bounds__(256) void wscale_kernel(const float *__restrict__ w
     }
 }
 
-// W [out][in] (torch Conv1d weight) -> three fp16 planes hi, mid, lo of
-// W * 2^s = hi + mid + lo (33 significant bits: every fp32 weight exactly) in
-// MFMA-fragment blocks (w3_index, pdsc_internal.hpp): block (t, ks) = outputs
-// 32t..32t+31 x the 16 inputs of k-step ks, planes hi / mid / lo of 1 KiB
+// W [out][in] (torch Conv1d weight) -> W_PLANES fp16 planes hi, mid (, lo) of
+// W * 2^s ~= hi + mid (22 significant bits; with lo: 33, every fp32 weight
+// exactly) in MFMA-fragment blocks (w3_index, pdsc_internal.hpp): block (t, ks)
+// = outputs 32t..32t+31 x the 16 inputs of k-step ks, planes of 1 KiB
 // each, lane (h, n)'s 16 B = positions 8h .. 8h+7 of output 32t + n in qk_pos
 // order (bits 2 and 3 of the input index swapped: inputs {4h..4h+3,
 // 8+4h..8+4h+3} of the k-step, exactly the channels a transposed product's
@@ -86,7 +86,7 @@ __global__ void pack_dense_kernel(const float *__restrict__ w, const float *__re
         const size_t d = w3_index(o, c, in);
         wd[d] = hi;
         wd[d + 512] = mid;
-        wd[d + 1024] = (_Float16)(r1 - (float)mid);
+        if (W_PLANES == 3) wd[d + 1024] = (_Float16)(r1 - (float)mid);
     }
     if (i < out) {
         db[i] = b[i];
@@ -403,7 +403,7 @@ constexpr int IN_LIMIT = 128;  // layer0 input width supported (datasets/ThreeDM
 // activations are read with the same map, so the products pair up).
 template <int IN, bool F32> struct WPanel;
 template <int IN> struct WPanel<IN, false> {
-    f16x8 h[IN / 16], m[IN / 16], l[IN / 16];
+    f16x8 h[IN / 16], m[IN / 16], l[W_PLANES == 3 ? IN / 16 : 1];  // (l: the 3-plane build only)
 };
 template <int IN> struct WPanel<IN, true> {
     f32x4 w[IN / 8];
@@ -422,7 +422,7 @@ PDSC_DEV void load_wpanel(const float *__restrict__ pk, const DenseOff &off, int
         for (int ks = 0; ks < IN / 16; ++ks) {
             p.h[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK);
             p.m[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK + 512);
-            p.l[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK + 1024);
+            if constexpr (W_PLANES == 3) p.l[ks] = *reinterpret_cast<const f16x8 *>(W + ks * W3_BLOCK + 1024);
         }
     }
 }
@@ -468,7 +468,7 @@ PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, 
             for (int i = 0; i < NRT; ++i) {
                 f16x8 xh, xl;
                 split8(xp + i * 32 * xstr + 16 * ks, h, xh, xl);
-                acc[i] = mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[ks], acc[i]);
+                acc[i] = mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[W_PLANES == 3 ? ks : 0], acc[i]);
             }
         }
     }
@@ -551,8 +551,8 @@ PDSC_DEV void dense_split(const char *Xs, const WPanel<CH, false> &wp, const flo
             const char *xr = Xs + r * XS_ROWB + 16 * ((2 * ks + h) ^ (r & 15));
             const f16x8 xh = *reinterpret_cast<const f16x8 *>(xr);
             const f16x8 xl = *reinterpret_cast<const f16x8 *>(xr + CH * 2);
-            acc[i] = MODE == SPLIT_V ? mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[ks], acc[i])
-                                     : mfma_w3x(wp.h[ks], wp.m[ks], wp.l[ks], xh, xl, acc[i]);
+            acc[i] = MODE == SPLIT_V ? mfma_xw3(xh, xl, wp.h[ks], wp.m[ks], wp.l[W_PLANES == 3 ? ks : 0], acc[i])
+                                     : mfma_w3x(wp.h[ks], wp.m[ks], wp.l[W_PLANES == 3 ? ks : 0], xh, xl, acc[i]);
         }
     }
     const float inv = pk[off.scale];
@@ -938,7 +938,7 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 // B = weights) to come out in the attention's V-tile layout.
 //
 // Weights: the kernel's layers are cut into chunks of <= PW2_CB weight blocks
-// (w3_index: one block = 32 outputs x 16 inputs x 3 planes = 3 KiB,
+// (w3_index: one block = 32 outputs x 16 inputs x W_PLANES planes of 1 KiB,
 // contiguous per chunk), listed in consumption order by the host (W2Sched).
 // Chunks are copied into a 2-slot LDS ring by LDS-DMA and shared by the
 // workgroup's waves: right after the barrier that retires chunk c, chunk c + 2
@@ -953,8 +953,13 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 #endif
 constexpr int PW2_W = PW2_WAVES;                      // waves per workgroup (32 points each)
 constexpr int PW2_OCC = PW2_W >= 8 ? 1 : 2;           // workgroups per CU (<= 256 VGPRs: 2 waves per SIMD)
-constexpr int PW2_CB = 8;                             // blocks per chunk (24 KiB)
-constexpr int PW2_BLKB = 3 * 1024;                    // bytes per block (3 planes)
+// 16 two-plane blocks = 32 KiB chunks (r04, A/B: -0.7 % per step at 128 x 1000
+// against 8, equal at 8 x 5000 and one pair): half the chunk barriers per chain
+#ifndef PW2_CHUNK_BLOCKS
+#define PW2_CHUNK_BLOCKS 16
+#endif
+constexpr int PW2_CB = PW2_CHUNK_BLOCKS;              // blocks per chunk (W_PLANES KiB each)
+constexpr int PW2_BLKB = W_PLANES * 1024;             // bytes per block (W_PLANES planes)
 constexpr int PW2_SLOT = PW2_CB * PW2_BLKB;
 constexpr int PW2_PTS = PW2_W * 32;
 constexpr int PW2_COEF = 1536;                        // floats of epilogue coefficients in LDS
@@ -978,7 +983,7 @@ static void w2_sched_add(W2Sched &S, const DenseOff &o, int in, int out) {
     const int nks = in / 16, nt = w2_nt(in, out);
     for (int c = 0; c < out / 32 / nt; ++c) {
         S.off[S.n] = (uint32_t)(2 * o.w + (size_t)c * nt * nks * W3_BLOCK);
-        S.np[S.n] = 3 * nt * nks;
+        S.np[S.n] = W_PLANES * nt * nks;
         ++S.n;
     }
 }
@@ -1020,7 +1025,7 @@ PDSC_DEV void w2_sync(bool active) {
 PDSC_DEV void w2_frag(const char *bp, f16x8 (&w)[3]) {
     w[0] = *reinterpret_cast<const f16x8 *>(bp);
     w[1] = *reinterpret_cast<const f16x8 *>(bp + 1024);
-    w[2] = *reinterpret_cast<const f16x8 *>(bp + 2048);
+    if constexpr (W_PLANES == 3) w[2] = *reinterpret_cast<const f16x8 *>(bp + 2048);
 }
 
 // acc[t0 + t] += W_t X over the chunk's NT tiles x NKS k-steps (TRANS: A = W,

@@ -41,12 +41,24 @@ __host__ __device__ inline size_t mfrag_floats(int N) {
 __host__ __device__ inline size_t mfrag_off(int qt, int kt, int nt) { return ((size_t)qt * nt + kt) * (MPACK_T * MPACK_T); }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Three-plane weight blocks: block (t, ks) = 32 outputs x one 16-input k-step,
-// planes hi / mid / lo of 64 lanes x 8 halfs (1 KiB) each, blocks t-major.
+// fp16 planes per packed 1x1-conv weight (3xfp16 mode): 2 = hi + mid (22
+// significant bits, products wh.xh + wh.xl + wm.xh: 3 MFMAs, as the attention's);
+// 3 = hi + mid + lo (every fp32 weight exactly, 4 MFMAs; the r01-r03 format,
+// kept as a build option for A/B: -DPDSC_W_PLANES=3).  r04 measured both on the
+// goldens (tools/emulate_conv.py): the same error class, inside the fp32
+// realisations' noise.
+#ifndef PDSC_W_PLANES
+#define PDSC_W_PLANES 2
+#endif
+constexpr int W_PLANES = PDSC_W_PLANES;
+static_assert(W_PLANES == 2 || W_PLANES == 3, "weight planes");
+
+// Weight blocks: block (t, ks) = 32 outputs x one 16-input k-step, planes
+// hi / mid (/ lo) of 64 lanes x 8 halfs (1 KiB) each, blocks t-major.
 // Element (o, c) of plane p sits at w3_index(o, c, in) + 512 p (halfs), with
 // lane (h, n), n = o % 32, holding positions 8h .. 8h+7 of the k-step in
 // qk_pos order (bits 2 and 3 of c % 16 swapped).
-constexpr int W3_BLOCK = 3 * 512;  // halfs per block
+constexpr int W3_BLOCK = W_PLANES * 512;  // halfs per block
 __host__ __device__ inline size_t w3_index(int o, int c, int in) {
     const int t = o >> 5, n = o & 31, ks = c >> 4, q = c & 15;
     const int pos = (q & ~12) | ((q & 4) << 1) | ((q & 8) >> 1);
@@ -58,9 +70,9 @@ __host__ __device__ inline size_t w3_index(int o, int c, int in) {
 //   W  : OUT*IN floats in MFMA fragment order:
 //        Wpk[((jt*(IN/8) + g)*64 + lane)*4 + e] = W[jt*32 + (lane&31)][(lane>>5)*(IN/2) + 4g + e]
 //   bias[OUT], alpha[OUT], beta[OUT]   (alpha=1, beta=0 when no BN)
-// A dense layer in the packed blob: W as three fp16 planes (hi, mid, lo: W * 2^s
-// = hi + mid + lo, s chosen per layer so max|W| 2^s <= 2^14) in MFMA-fragment
-// blocks (w3_index) occupying 1.5*out*in floats at w -- or, for
+// A dense layer in the packed blob: W as W_PLANES fp16 planes (hi, mid[, lo] of
+// W * 2^s, s chosen per layer so max|W| 2^s <= 2^14) in MFMA-fragment blocks
+// (w3_index) occupying W_PLANES/2*out*in floats at w (at least out*in) -- or, for
 // PDSC_PRECISION_F32, W itself fp32 [out][in] in the first out*in of them --
 // then bias, alpha, beta [out] and scale = {2^-s, 2^s}.
 struct DenseOff {
@@ -85,7 +97,7 @@ struct PackLayout {
 inline DenseOff dense_at(size_t &o, int in, int out) {
     DenseOff d;
     d.w = o;
-    o += (size_t)out * in * 3 / 2;
+    o += (size_t)out * in * (W_PLANES > 2 ? W_PLANES : 2) / 2;
     d.bias = o;
     o += out;
     d.alpha = o;

@@ -9,6 +9,9 @@
 // which is deterministic and equals torch's order whenever scores are distinct.
 // Both kernels are O(N^2) compare loops over LDS-staged tiles (VALU bound, a
 // few microseconds at N = 5000).
+#include <algorithm>
+#include <cstdlib>
+
 #include "pdsc_internal.hpp"
 
 namespace pdsc {
@@ -115,11 +118,151 @@ __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict_
     }
 }
 
+// ------------------------------------------------------------------ sorted forms
+// Both O(N^2) compare kernels above have an O(N log^2 N + N w) form for pairs of
+// up to SORT_MAX points, one workgroup of 1024 threads per pair (per pair and
+// 1024-row chunk for the NMS): a bitonic sort of 64-bit keys in LDS.
+//   seed ranking: keys (descending score, ascending index) -- the top S of the
+//   sorted list IS the rank order above, bit for bit (-0 is keyed as +0, so the
+//   two tie as they compare equal);
+//   NMS: keys (ascending x, index); row i compares only the points whose x lies
+//   within 1.0625 sqrt(R2) of its own (found by binary search).  Any j farther
+//   than that has |fl(x_i - x_j)| >= 1.0625 sqrt(R2) (1 - 2^-24), so its
+//   squared distance -- a sum of non-negative terms, rounding monotone -- is
+//   >= 1.12 R2 >= R2: the excluded compares are exactly the ones that cannot
+//   violate.  A pair with a non-finite coordinate (NaN distances count as
+//   within the radius) or a non-finite / NaN window scans every j.
+constexpr int SORT_MAX = 8192;     // seed ranking: 64-bit keys, 64 KiB
+constexpr int NMS_SORT_MAX = 5120;  // NMS: keys + sorted points (x, y, z, conf), 144 KiB
+constexpr int SORT_NT = 1024;
+
+PDSC_DEV void bitonic_sort_u64(unsigned long long *k, int P, int tid) {
+    for (int size = 2; size <= P; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int t = tid; t < P / 2; t += SORT_NT) {
+                const int i = 2 * t - (t & (stride - 1)), j = i + stride;  // the t-th pair at this stride
+                const unsigned long long a = k[i], b = k[j];
+                if ((a > b) == ((i & size) == 0)) {
+                    k[i] = b;
+                    k[j] = a;
+                }
+            }
+        }
+    __syncthreads();
+}
+
+// order-preserving uint32 of a float (ascending); -0 keyed as +0
+PDSC_DEV uint32_t float_key(float f) {
+    const uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+PDSC_DEV int pow2_at_least(int n) {
+    int P = 64;
+    while (P < n) P <<= 1;
+    return P;
+}
+
+__global__ __launch_bounds__(SORT_NT) void seed_rank_sort_kernel(const float *__restrict__ conf,
+                                                                 const float *__restrict__ lm, int Nstr, int Sstr,
+                                                                 int *__restrict__ seeds, Ragged rg) {
+    extern __shared__ unsigned long long skeys[];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    const int P = pow2_at_least(N);
+    conf += (size_t)b * Nstr;
+    lm += (size_t)b * Nstr;
+    for (int i = tid; i < P; i += SORT_NT)
+        skeys[i] = i < N ? ((unsigned long long)~float_key(conf[i] * lm[i]) << 32) | (unsigned)i  // (:217)
+                         : ~0ull;
+    bitonic_sort_u64(skeys, P, tid);
+    for (int r = tid; r < S; r += SORT_NT) seeds[(size_t)b * Sstr + r] = (int)(unsigned)skeys[r];
+}
+
+__global__ __launch_bounds__(SORT_NT) void local_max_sort_kernel(const float *__restrict__ src,
+                                                                 const float *__restrict__ conf, int Nstr, float R2,
+                                                                 float *__restrict__ lm, Ragged rg) {
+    extern __shared__ unsigned long long skeys[];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int N = rg.n(b, Nstr);
+    if (blockIdx.x * SORT_NT >= N) return;  // workgroup-uniform (ragged pairs)
+    const int P = pow2_at_least(N);
+    f32x4 *sp = reinterpret_cast<f32x4 *>(skeys + P);  // points in ascending-x order: (x, y, z, conf)
+    src += (size_t)b * Nstr * 3;
+    conf += (size_t)b * Nstr;
+    int bad = 0;
+    for (int i = tid; i < P; i += SORT_NT) {
+        if (i < N) {
+            const float x = src[3 * i], y = src[3 * i + 1], z = src[3 * i + 2];
+            bad |= !(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z));
+            skeys[i] = ((unsigned long long)float_key(x) << 32) | (unsigned)i;
+        } else {
+            skeys[i] = ~0ull;
+        }
+    }
+    bad = __syncthreads_or(bad);
+    bitonic_sort_u64(skeys, P, tid);
+    for (int q = tid; q < N; q += SORT_NT) {
+        const int i = (int)(unsigned)skeys[q];
+        sp[q] = f32x4{src[3 * i], src[3 * i + 1], src[3 * i + 2], conf[i]};
+    }
+    __syncthreads();
+    const int q = blockIdx.x * SORT_NT + tid;  // this thread's row, in sorted order
+    if (q >= N) return;
+    const f32x4 pi = sp[q];
+    const double W = 1.0625 * sqrt((double)R2);
+    int lo = 0, hi = N;  // the window [lo, hi) of sorted positions (everything when it cannot be trusted)
+    if (!bad && W <= 1e300) {
+        const double xl = (double)pi[0] - W, xh = (double)pi[0] + W;
+        int a = 0, c = q;  // first position with x >= xl
+        while (a < c) {
+            const int m = (a + c) >> 1;
+            if ((double)sp[m][0] >= xl) c = m; else a = m + 1;
+        }
+        lo = a;
+        a = q + 1;
+        c = N;  // first position with x > xh
+        while (a < c) {
+            const int m = (a + c) >> 1;
+            if ((double)sp[m][0] > xh) c = m; else a = m + 1;
+        }
+        hi = a;
+    }
+    // violation: c_i < c_j and !(|s_i - s_j| >= R) -- the compare of local_max_kernel
+    bool viol = false;
+    for (int j = lo; j < hi; ++j) {
+        const f32x4 pj = sp[j];
+        const float x = sqdist3(pi[0], pi[1], pi[2], pj[0], pj[1], pj[2]);
+        viol |= (pi[3] < pj[3]) & !(x >= R2);
+    }
+    lm[(size_t)b * Nstr + (int)(unsigned)skeys[q]] = viol ? 0.0f : 1.0f;
+}
+
 static bool seed_small(int B, int N) { return (long)B * ((N + 63) / 64) < 512; }
+
+// The sorted forms are opt-in (A/B knob PDSC_SEED_SORT=1, measurement only):
+// r04 measured them slower than the compare kernels at every bench shape --
+// 8 x 5000 forward 4.60 vs 4.51 ms, one N = 1000 pair 0.467 vs 0.441 ms, equal
+// at 128 x 1000 -- one 1024-thread workgroup per pair sorts 1024-8192 keys in
+// 55-91 barrier-separated steps, against the compare kernels' hundreds of
+// workgroups.
+static bool seed_sort_on() {
+    static const bool on = [] {
+        const char *e = getenv("PDSC_SEED_SORT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+static size_t sort_lds(int N) { return (size_t)std::max(64, 1 << (32 - __builtin_clz((unsigned)std::max(N - 1, 1)))) * 8; }
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s, Ragged rg) {
-    if (seed_small(B, N))
+    if (seed_sort_on() && N <= NMS_SORT_MAX) {
+        const size_t lds = sort_lds(N) + (size_t)N * sizeof(f32x4);
+        hipLaunchKernelGGL(local_max_sort_kernel, dim3((N + SORT_NT - 1) / SORT_NT, B), dim3(SORT_NT), lds, s, src, conf,
+                           N, sqrt_ge_threshold(radius), lm, rg);
+    } else if (seed_small(B, N))
         hipLaunchKernelGGL(local_max_kernel<16>, dim3((N + 15) / 16, B), dim3(256), 0, s, src, conf, N,
                            sqrt_ge_threshold(radius), lm, rg);
     else
@@ -130,7 +273,9 @@ hipError_t launch_local_max(const float *src, const float *conf, int B, int N, f
 
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
                             hipStream_t s, Ragged rg) {
-    if (seed_small(B, N))
+    if (seed_sort_on() && N <= SORT_MAX)
+        hipLaunchKernelGGL(seed_rank_sort_kernel, dim3(B), dim3(SORT_NT), sort_lds(N), s, conf, lm, N, S, seeds, rg);
+    else if (seed_small(B, N))
         hipLaunchKernelGGL(seed_rank_kernel<16>, dim3((N + 15) / 16, B), dim3(256), 0, s, conf, lm, N, S, seeds, rg);
     else
         hipLaunchKernelGGL(seed_rank_kernel<64>, dim3((N + 63) / 64, B), dim3(256), 0, s, conf, lm, N, S, seeds, rg);

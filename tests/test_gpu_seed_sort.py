@@ -1,0 +1,51 @@
+"""The opt-in sorted forms of a5 (seeds.hip: bitonic-sorted NMS window and seed
+ranking, knob PDSC_SEED_SORT=1, measurement only) give exactly the compare
+kernels' bits: is_local_max and the seed list, on tie-heavy scores, -0 / +0
+scores and duplicate points (run with -m gpu)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(3, 1000, 100, 0.1), (2, 5000, 500, 0.1), (1, 777, 77, 0.6), (4, 64, 6, 0.05)]
+
+
+def _inputs(B, N, seed):
+    rng = np.random.RandomState(seed)
+    src = (rng.rand(B, N, 3) * 3).astype(np.float32)
+    idx = np.arange(0, N - 1, 17)
+    src[:, idx] = src[:, idx + 1]  # duplicate points
+    conf = np.round(rng.randn(B, N) * 4).astype(np.float32)  # many exact ties
+    conf[:, ::5] = 0.0
+    conf[:, 1::11] = -0.0
+    return src, conf
+
+
+def _dump(path):
+    from pointdsc_amd import kernels
+    dev = torch.device("cuda:0")
+    out = {}
+    for i, (B, N, S, R) in enumerate(CASES):
+        src, conf = _inputs(B, N, 100 + i)
+        seeds, lm = kernels.pick_seeds(torch.from_numpy(src).to(dev), torch.from_numpy(conf).to(dev), R, S)
+        out[f"seeds{i}"], out[f"lm{i}"] = seeds.cpu().numpy(), lm.cpu().numpy()
+    np.savez(path, **out)
+
+
+def test_sorted_seed_kernels_bit_identical(gpu_device, tmp_path):
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for knob in ("0", "1"):
+        path = tmp_path / f"seeds_{knob}.npz"
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_seed_sort as t; t._dump({str(path)!r})"
+        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PDSC_SEED_SORT=knob), check=True,
+                       timeout=240)
+        res[knob] = np.load(path)
+    for k in res["0"].files:
+        assert np.array_equal(res["0"][k], res["1"][k]), k

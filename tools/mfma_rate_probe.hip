@@ -54,12 +54,16 @@ __global__ __launch_bounds__(256, 1) void probe_lds(const f16x8 *in, float *out,
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256, 1) void probe(const f16x8 *in, float *out, unsigned long long *cyc, int iters) {
+template <int MODE, int NT = 256>
+__global__ __launch_bounds__(NT, 1) void probe(const f16x8 *in, float *out, unsigned long long *cyc, int iters) {
     asm volatile("" ::: "a0", "a255");
     f16x8 a = in[threadIdx.x], b = in[threadIdx.x + 256];
     f32x16 acc = {};
-    float x = (float)threadIdx.x, y = 1.0001f;
+    float x = (float)threadIdx.x, y = 1.0001f, z = 0.5f;
+    f16x8 dsv;
+    const unsigned dsa = (threadIdx.x & 63) * 16;
+    __shared__ char lds_[65536];
+    if (threadIdx.x == 0) lds_[0] = 0;
     asm volatile("v_accvgpr_write_b32 a128, 0\n v_accvgpr_write_b32 a129, 0\n v_accvgpr_write_b32 a130, 0\n v_accvgpr_write_b32 a131, 0");
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < iters; ++it) {
@@ -80,6 +84,27 @@ __global__ __launch_bounds__(256, 1) void probe(const f16x8 *in, float *out, uns
             } else if (MODE == 5) {  // PV + ds_read-ish filler: 2 VALU
                 asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
                 asm volatile("v_fma_f32 %0, %0, %1, %1\n v_fma_f32 %0, %0, %1, %1\n v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(y));
+            } else if (MODE == 6) {  // PV + one exp
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+                asm volatile("v_exp_f32 %0, %0" : "+v"(x));
+            } else if (MODE == 7) {  // PV + 4 independent fma
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+                asm volatile("v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2\n v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2" : "+v"(x), "+v"(z) : "v"(y));
+            } else if (MODE == 8) {  // PV + 8 independent fma
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+                asm volatile("v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2\n v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2\n"
+                             "v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2\n v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2" : "+v"(x), "+v"(z) : "v"(y));
+            } else if (MODE == 9) {  // PV + 2 independent exp
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+                asm volatile("v_exp_f32 %0, %0\n v_exp_f32 %1, %1" : "+v"(x), "+v"(z));
+            } else if (MODE == 10) {  // PV + 16 independent fma
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                asm volatile("v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2\n v_fma_f32 %0, %0, %2, %2\n v_fma_f32 %1, %1, %2, %2" : "+v"(x), "+v"(z) : "v"(y));
+            } else if (MODE == 11) {  // PV + 2 ds_read_b128 (independent, no wait)
+                asm volatile("v_mfma_f32_32x32x16_f16 a[0:15], %0, %1, a[0:15]" ::"v"(a), "v"(b));
+                asm volatile("ds_read_b128 %0, %1\n ds_read_b128 %0, %1 offset:1024" : "=v"(dsv) : "v"(dsa));
             }
         }
     }
@@ -87,8 +112,9 @@ __global__ __launch_bounds__(256, 1) void probe(const f16x8 *in, float *out, uns
     asm volatile("s_nop 15\n s_nop 15");
     float r;
     asm volatile("v_accvgpr_read_b32 %0, a5" : "=v"(r));
-    out[blockIdx.x * 256 + threadIdx.x] = r + acc[3] + x + y;
-    if (threadIdx.x % 64 == 0) {
+    asm volatile("s_waitcnt lgkmcnt(0)");
+    out[blockIdx.x * NT + threadIdx.x] = r + acc[3] + x + y + z + (float)dsv[0];
+    if (threadIdx.x % 64 == 0 && threadIdx.x < 256) {
         cyc[blockIdx.x * 4 + threadIdx.x / 64] = t1 - t0;
         cyc[4096 + blockIdx.x * 4 + threadIdx.x / 64] = r1 - r0;
     }
@@ -109,11 +135,11 @@ int main() {
         }
         hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
     }
-    hipMalloc(&out, G * 256 * 4);
+    hipMalloc(&out, G * 512 * 4);
     hipMalloc(&cyc, 8192 * 8);
     std::vector<unsigned long long> h(8192);
-    auto run = [&](auto k, const char *name) {
-        for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k, dim3(G), dim3(256), 0, 0, in, out, cyc, iters);
+    auto run = [&](auto k, const char *name, int nt = 256) {
+        for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k, dim3(G), dim3(nt), 0, 0, in, out, cyc, iters);
         hipDeviceSynchronize();
         hipMemcpy(h.data(), cyc, h.size() * 8, hipMemcpyDeviceToHost);
         std::vector<unsigned long long> s(h.begin(), h.begin() + G * 4);
@@ -131,6 +157,15 @@ int main() {
     run(probe<3>, "PV + 1 fma");
     run(probe<4>, "PV + exp add cvt mix mix");
     run(probe<5>, "PV + 3 dependent fma");
+    run(probe<6>, "PV + 1 exp");
+    run(probe<9>, "PV + 2 independent exp");
+    run(probe<7>, "PV + 4 independent fma");
+    run(probe<8>, "PV + 8 independent fma");
+    run(probe<10>, "PV + 16 independent fma");
+    run(probe<11>, "PV + 2 ds_read_b128");
+    run(probe<0, 512>, "2 waves/SIMD: PV (per wave)", 512);
+    run(probe<4, 512>, "2 waves/SIMD: PV + exp add cvt mix mix", 512);
+    run(probe<8, 512>, "2 waves/SIMD: PV + 8 independent fma", 512);
     run(probe_lds<0>, "PV, V from LDS 2 frags ahead");
     run(probe_lds<1>, "PV, V from LDS + 1 fma");
     return 0;
