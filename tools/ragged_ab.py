@@ -1,0 +1,68 @@
+"""Where the ragged batch loses (diagnostic): ms per forward of
+  uniform   128 x N=1000 through the batched forward,
+  padded    the same 128 x 1000 pairs through the ragged entry at the ragged
+            batch's row stride (every count 1000, N_max 1285),
+  ragged    bench.py's ragged leg: 128 pairs, N_b ~ U[700, 1300] (seeded as there),
+  ragged1k  the same sizes scaled to mean 1000 exactly is not possible, so the
+            ragged batch's correspondences / forward time is printed as corr/s.
+Usage: python tools/ragged_ab.py [reps]"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+
+def main():
+    from pointdsc_amd import kernels
+    from pointdsc_amd.PointDSC import PointDSC
+    from pointdsc_amd.synthetic import BENCH_CLS, PRESETS, synthetic_pair, trained_state_dict
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    dev = torch.device("cuda:0")
+    p = PRESETS["3dmatch"]
+    m = PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40, nms_radius=p["nms_radius"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict("3dmatch", 12, *BENCH_CLS).items()})
+    m = m.to(dev).eval()
+    cfg, pk = m.pdsc_config(), m.packed_weights()
+    rng = np.random.RandomState(1234)
+    P = 128
+    sizes = rng.randint(700, 1301, size=P).tolist()
+    ps = [synthetic_pair(n, 7000 + i) for i, n in enumerate(sizes)]
+    Nmax = max(sizes)
+
+    def pad(key, n_rows):
+        out = np.zeros((P, Nmax, ps[0][key].shape[1]), np.float32)
+        for b, q in enumerate(ps):
+            out[b, :min(n_rows[b], len(q[key]))] = q[key][:n_rows[b]]
+        return torch.from_numpy(out).to(dev)
+
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    pu = [synthetic_pair(1000, 7000 + i) for i in range(P)]
+    cu, su, tu = (torch.from_numpy(np.stack([q[k] for q in pu])).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    t_uni = timeit(lambda: kernels.forward_testing(cfg, pk, cu, su, tu, check_range=False))
+    cp, sp_, tp = (torch.zeros((P, Nmax, x.shape[2]), device=dev) for x in (cu, su, tu))
+    cp[:, :1000], sp_[:, :1000], tp[:, :1000] = cu, su, tu
+    t_pad = timeit(lambda: kernels.forward_ragged(cfg, pk, cp, sp_, tp, [1000] * P, check_range=False))
+    rows = sizes
+    cr, sr, tr = pad("corr_pos", rows), pad("src_keypts", rows), pad("tgt_keypts", rows)
+    t_rag = timeit(lambda: kernels.forward_ragged(cfg, pk, cr, sr, tr, sizes, check_range=False))
+    print(f"{os.environ.get('AB_TAG', '')} uniform {t_uni:.3f} ms ({P * 1000 / t_uni * 1e3:.3g} corr/s) | "
+          f"padded-to-{Nmax} {t_pad:.3f} ms | ragged {t_rag:.3f} ms ({sum(sizes) / t_rag * 1e3:.3g} corr/s, "
+          f"sum n^2 / (128 x 1e6) = {sum(n * n for n in sizes) / (P * 1e6):.3f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
