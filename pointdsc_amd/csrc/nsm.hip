@@ -531,16 +531,16 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
     unsigned flags = 0;
     __builtin_amdgcn_wave_barrier();
     for (int t = 0; t < T; ++t) {
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        // four partial sums as two packed pairs: v_pk_fma_f32, two lanes' worth of
+        // fma per instruction, the same arithmetic per component
+        f32x2 acc01 = {0.0f, 0.0f}, acc23 = {0.0f, 0.0f};
 #pragma unroll
         for (int c = 0; c < KC; c += 4) {
             const f32x4 vv = *reinterpret_cast<const f32x4 *>(&vbuf[c]);
-            acc[0] = __builtin_fmaf(trow[c], vv[0], acc[0]);
-            acc[1] = __builtin_fmaf(trow[c + 1], vv[1], acc[1]);
-            acc[2] = __builtin_fmaf(trow[c + 2], vv[2], acc[2]);
-            acc[3] = __builtin_fmaf(trow[c + 3], vv[3], acc[3]);
+            acc01 = __builtin_elementwise_fma(f32x2{trow[c], trow[c + 1]}, f32x2{vv[0], vv[1]}, acc01);
+            acc23 = __builtin_elementwise_fma(f32x2{trow[c + 2], trow[c + 3]}, f32x2{vv[2], vv[3]}, acc23);
         }
-        float nv = (acc[0] + acc[1]) + (acc[2] + acc[3]);   // (T v)_a  (bmm, :352)
+        float nv = (acc01[0] + acc01[1]) + (acc23[0] + acc23[1]);   // (T v)_a  (bmm, :352)
         const float nrm = sqrtf(wave_sum_dpp(nv * nv));  // no LDS round trip per iterate
         nv = nv / (nrm + 1e-6f);                              // :353
         const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
@@ -743,7 +743,10 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         const f32x4 pc0 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR);
         const f32x4 pc1 = *reinterpret_cast<const f32x4 *>(P + c * NSM_PSTR + 4);
         // correctly rounded '/' and sqrtf through their fma-corrected forms
-        // (pdsc_common.hpp; exact for normal operands, within 1 ulp below 2^-96)
+        // (pdsc_common.hpp; exact for normal operands, within 1 ulp below 2^-96).
+        // (r04: the hardware square root and a reciprocal multiply in the H3 build,
+        // -22 VALU per pair, flipped one borderline pair of the recall-parity
+        // proxy -- test_recall_parity_synthetic -- so both modes keep these.)
         const float fm = fmaxf(1.0f - cr_div(1.0f - g, sig2, rsig2), 0.0f);  // :259
         float dx = pa0[0] - pc0[0], dy = pa0[1] - pc0[1], dz = pa0[2] - pc0[2];
         const float ds = cr_sqrt((dx * dx + dy * dy) + dz * dz);    // :268
