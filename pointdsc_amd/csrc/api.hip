@@ -551,7 +551,9 @@ int32_t pdsc_pick_seeds(const float *src, const float *conf, int32_t B, int32_t 
 // a6 (:250-252) for the forwards: knn [B][S][k]; dist [B][S][N] scratch
 int run_seed_knn(const float *normed, const _Float16 *normed_s, bool f32, const int *seeds, int B, int N, int S,
                  int k, float *dist, int *knn, hipStream_t s, Ragged rg = {}) {
-    HIPCHK(hipMemsetAsync(knn, 0, sizeof(int) * B * S * k, s));
+    // (no zero fill of knn: knn_select writes all k entries of every seed row it
+    // owns -- ranks 1 .. k of k + 1 distinct (key, index) candidates -- and the
+    // rows past a ragged pair's own seeds are never read; readers clamp indices)
     if (f32) {
         HIPCHK(launch_knn_dist_f32(normed, seeds, B, N, S, dist, s, rg));
     } else {
