@@ -313,6 +313,7 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int slots) {
 // (consecutive workgroup ids round-robin over the 8 XCDs).
 struct AttnBlock {
     int b, qb, split;
+    int st0 = 0, st1 = -1;  // key tiles [st0, st1) when st1 >= 0 (attention_w64_sk_kernel), else the split's
 };
 PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
     const int G = g.B * g.nqb * g.nsplit;

@@ -204,7 +204,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     const int h = lane >> 5;
     const int q0 = qb * W64_QPB + wave * W64_QW;  // block u: queries q0 + 32 u ..
     const int nst = (N + H3_TILE - 1) / H3_TILE;
-    const int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
+    const int st0 = blk.st1 >= 0 ? blk.st0 : split * g.sps, st1 = blk.st1 >= 0 ? blk.st1 : min(nst, st0 + g.sps);
 
     const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
     const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
@@ -658,20 +658,13 @@ template <int U> PDSC_DEV void w64_read_o(f32x16 (&O)[4]) {
     });
 }
 
-// Split-K attention with 64-query waves: partials as attention_h3_kernel.
-template <bool XCD>
-__global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
-    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
-    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
-    float *__restrict__ ml) {
-    extern __shared__ __attribute__((aligned(16))) char w64smem[];
-    const AttnBlock blk = attention_h3_block(g, XCD);
-    if (blk.qb * W64_QPB >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
-    const int b = blk.b, split = blk.split, Npad = g.Npad;
-    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5;
-    float m_run[2], l_run[2];
-    attention_w64_core(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
-    const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
+// This workgroup's partial (split blk.split of query block blk.qb): O^T rows in
+// the fragment-block tiling of attention_h3_kernel, m (natural-log units) and l.
+PDSC_DEV void w64_store_partial(const AttnGridH3 &g, const AttnBlock &blk, float *__restrict__ opart,
+                                float *__restrict__ ml, int wave, int lane, const float (&m_run)[2],
+                                const float (&l_run)[2]) {
+    const int Npad = g.Npad, h = lane >> 5;
+    const size_t obase = (size_t)(blk.b * g.nsplit + blk.split) * Npad;
     static_for<2>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const int q0 = blk.qb * W64_QPB + wave * W64_QW + 32 * u, qq = q0 + (lane & 31);
@@ -691,6 +684,83 @@ __global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
             }
         }
     });
+}
+
+// Split-K attention with 64-query waves: partials as attention_h3_kernel.
+template <bool XCD>
+__global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
+    float *__restrict__ ml) {
+    extern __shared__ __attribute__((aligned(16))) char w64smem[];
+    const AttnBlock blk = attention_h3_block(g, XCD);
+    if (blk.qb * W64_QPB >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    float m_run[2], l_run[2];
+    attention_w64_core(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
+    w64_store_partial(g, blk, opart, ml, wave, lane, m_run, l_run);
+}
+
+// ---- stream-K form (uniform batches) ------------------------------------------
+// The split grid runs ceil(B nqb nsplit / slots) rounds of whole splits: 8 x 5000
+// is 480 workgroups of 53 key tiles on 256 CUs, a second round 7/8 full.  Here
+// one round of `nwg` workgroups (one per CU) shares the T = B nqb nst (query
+// block, key tile) pairs evenly: logical workgroup w owns the block-major tiles
+// [w T / nwg, (w + 1) T / nwg), XCD-major (logical ids w .. of one XCD hold
+// consecutive tiles, so a pair's blocks stay in one L2).  Each maximal run of
+// those tiles inside one query block is a segment, stored as split
+// s = w - (owner of the block's first tile); the owner of the block's last tile
+// also writes the slots past its own as an empty split leaves them (O = 0,
+// m = -inf, l = 0), so the combine reads nsplit slots as before.
+__host__ __device__ inline int w64_sk_owner(long x, long T, int nwg) { return (int)(((x + 1) * nwg - 1) / T); }
+inline int w64_sk_nsplit(int B, int nqb, int nst, int nwg) {
+    const long T = (long)B * nqb * nst;
+    int ns = 1;
+    for (long k = 0; k < (long)B * nqb; ++k)
+        ns = std::max(ns, w64_sk_owner(k * nst + nst - 1, T, nwg) - w64_sk_owner(k * nst, T, nwg) + 1);
+    return ns;
+}
+
+// split s of query block (b, qb) as an empty split leaves it
+PDSC_DEV void w64_zero_partial(const AttnGridH3 &g, int b, int qb, int s, float *__restrict__ opart,
+                               float *__restrict__ ml, int tid) {
+    const int Npad = g.Npad;
+    const size_t obase = (size_t)(b * g.nsplit + s) * Npad;
+    const int r0 = qb * W64_QPB, r1 = min(Npad, r0 + W64_QPB);  // rows (multiples of 32)
+    f32x4 *Ob = reinterpret_cast<f32x4 *>(opart + (obase + r0) * CH);
+    for (int i = tid; i < (r1 - r0) * CH / 4; i += W64_NW * 64) Ob[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int r = r0 + tid; r < r1; r += W64_NW * 64) {
+        ml[(obase + r) * 2] = -INFINITY;
+        ml[(obase + r) * 2 + 1] = 0.0f;
+    }
+}
+
+template <bool XCD>
+__global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_sk_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, int nwg, float *__restrict__ opart,
+    float *__restrict__ ml) {
+    extern __shared__ __attribute__((aligned(16))) char w64smem[];
+    int w = blockIdx.x;
+    if (XCD && (nwg & 7) == 0) w = (w & 7) * (nwg >> 3) + (w >> 3);
+    const int nst = (g.N + H3_TILE - 1) / H3_TILE;
+    const long T = (long)g.B * g.nqb * nst;
+    const long hi = (long)(w + 1) * T / nwg;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    for (long x = (long)w * T / nwg; x < hi;) {
+        const int k = (int)(x / nst);
+        const long k0 = (long)k * nst, x1 = min(hi, k0 + nst);
+        AttnBlock blk{k / g.nqb, k % g.nqb, w - w64_sk_owner(k0, T, nwg)};
+        blk.st0 = (int)(x - k0);
+        blk.st1 = (int)(x1 - k0);
+        __builtin_amdgcn_s_waitcnt(0x0070);  // the previous segment's stores: the core starts with none in flight
+        float m_run[2], l_run[2];
+        attention_w64_core(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
+        w64_store_partial(g, blk, opart, ml, wave, lane, m_run, l_run);
+        if (x1 == k0 + nst)
+            for (int s = blk.split + 1; s < g.nsplit; ++s) w64_zero_partial(g, blk.b, blk.qb, s, opart, ml, tid);
+        x = x1;
+    }
 }
 
 }  // namespace pdsc

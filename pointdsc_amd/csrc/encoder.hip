@@ -160,8 +160,31 @@ bool attention_w64(int B, int N, bool f32) {
     return mode == 1 || (long)B * ((N + W64_QPB - 1) / W64_QPB) >= 128;
 }
 
+// Stream-K workgroups for a uniform batch on the w64 path (attention_w64_sk_kernel,
+// one per CU), or 0 for the split grid: when one round of nwg workgroups of
+// ceil(T / nwg) tiles (+ ~2 tiles for a workgroup's second segment) beats the
+// split grid's rounds of sps tiles.  Knob PDSC_W64_SK=0: never (measurement only).
+static int w64_sk_wgs(int B, int N) {
+    static const int mode = [] {
+        const char *e = getenv("PDSC_W64_SK");
+        return e ? atoi(e) : 1;
+    }();
+    if (!mode) return 0;
+    const int nwg = att_target() / 2;
+    const AttnGridH3 g = w64_grid(B, N);
+    const int nst = (N + H3_TILE - 1) / H3_TILE;
+    const long T = (long)B * g.nqb * nst, rounds = ((long)B * g.nqb * g.nsplit + nwg - 1) / nwg;
+    return T >= 4L * nwg && (T + nwg - 1) / nwg + 2 < rounds * g.sps ? nwg : 0;
+}
+// the w64 plan's partial slots: the split grid's, or the stream-K segments' if more
+static int w64_nsplit(int B, int N) {
+    const AttnGridH3 g = w64_grid(B, N);
+    const int nwg = w64_sk_wgs(B, N);
+    return nwg ? std::max(g.nsplit, w64_sk_nsplit(B, g.nqb, (N + H3_TILE - 1) / H3_TILE, nwg)) : g.nsplit;
+}
+
 int attention_nsplit(int B, int N, bool f32, bool w64) {
-    return f32 ? f32_grid(B, N).nsplit : (w64 ? w64_grid(B, N).nsplit : prod_grid(B, N).nsplit);
+    return f32 ? f32_grid(B, N).nsplit : (w64 ? w64_nsplit(B, N) : prod_grid(B, N).nsplit);
 }
 
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
@@ -171,9 +194,17 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     if (m_layout == M_FRAG) {  // attention_w64 (H3 layouts, fragment-ordered M)
         if (f32) return hipErrorInvalidValue;
         AttnGridH3 g = w64_grid(B, N);
+        if (g.Npad != Npad || nsplit != w64_nsplit(B, N)) return hipErrorInvalidValue;
+        g.nsplit = nsplit;  // slots past the split grid's own: empty splits (st0 >= st1)
+        const int nwg = rg.nv ? 0 : w64_sk_wgs(B, N);
+        if (nwg) {
+            hipLaunchKernelGGL((attention_w64_sk_kernel<true>), dim3(nwg), dim3(W64_NW * 64), W64_LDS, s,
+                               static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
+                               static_cast<const _Float16 *>(v), vexp, M, g, nwg, opart, ml);
+            return hipGetLastError();
+        }
         g.nv = rg.nv;
         g.po = rg.po;
-        if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
         hipLaunchKernelGGL((attention_w64_kernel<true>), dim3(g.B * g.nqb * g.nsplit), dim3(W64_NW * 64), W64_LDS, s,
                            static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
                            static_cast<const _Float16 *>(v), vexp, M, g, opart, ml);
