@@ -1167,7 +1167,12 @@ PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restric
     for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     for (int s = 0; s < nsplit; ++s) {
         const size_t base = (size_t)(b * nsplit + s) * Npad + row;
-        const float w = expf(ml[base * 2] - mstar);
+        const float ms = ml[base * 2];
+        // an empty split (m = -inf: past a ragged pair's keys, or a stream-K slot past
+        // the block's segments, attention_w64.hpp) has w = 0: its O is not read
+        // (uniform over the wave's 32 rows, which share one query block)
+        if (ms == -INFINITY) continue;
+        const float w = expf(ms - mstar);
         L += w * ml[base * 2 + 1];
         const float *src = opart + (base - (row & 31)) * CH + 4 * lane;  // the tile's first block
 #pragma unroll

@@ -351,7 +351,10 @@ def test_fused_encoder_bit_identical(gpu_device, tmp_path):
     kept in registers) gives exactly the bits of the separate attention_h3 +
     pw2_mid launches (run in a child process with the PDSC_FUSE=0 knob): encoder
     features / confidences with dense M, and the whole forward with packed M; a
-    two-round headline-like batch and a 1.25-round one (320 workgroups)."""
+    two-round headline-like batch and a 1.25-round one (320 workgroups).  The
+    unfused child keeps the split grid (PDSC_W64_SK=0): its one key split per
+    query block is the fused kernel's arithmetic, where stream-K's segments
+    (40 x 1000: 3 per block) would combine in another fp32 order."""
     import ctypes
     import os
     import subprocess
@@ -364,7 +367,7 @@ def test_fused_encoder_bit_identical(gpu_device, tmp_path):
         assert fused.value == 1, (B, N)
         ours = _fusion_outputs(gpu_device, B, N)
         out = tmp_path / f"unfused_{B}_{N}.npz"
-        env = dict(os.environ, PDSC_FUSE="0")
+        env = dict(os.environ, PDSC_FUSE="0", PDSC_W64_SK="0")
         code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
                f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
         subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)

@@ -1,7 +1,7 @@
 """The opt-in sorted forms of a5 (seeds.hip: bitonic-sorted NMS window and seed
 ranking, knob PDSC_SEED_SORT=1, measurement only) give exactly the compare
 kernels' bits: is_local_max and the seed list, on tie-heavy scores, -0 / +0
-scores and duplicate points (run with -m gpu)."""
+scores, negative local maxima and duplicate points (run with -m gpu)."""
 import os
 import subprocess
 import sys
@@ -12,7 +12,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-CASES = [(3, 1000, 100, 0.1), (2, 5000, 500, 0.1), (1, 777, 77, 0.6), (4, 64, 6, 0.05)]
+CASES = [(3, 1000, 100, 0.1), (2, 5000, 500, 0.1), (1, 777, 77, 0.6), (4, 64, 6, 0.05), (1, 6000, 600, 1e-3),
+         (2, 3000, 300, 0.02)]
 
 
 def _inputs(B, N, seed):
@@ -37,15 +38,14 @@ def _dump(path):
     np.savez(path, **out)
 
 
-def test_sorted_seed_kernels_bit_identical(gpu_device, tmp_path):
+def test_seed_kernel_forms_bit_identical(gpu_device, tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for knob in ("0", "1"):
-        path = tmp_path / f"seeds_{knob}.npz"
+    for tag, env in (("full", dict(PDSC_SEED_SORT="0")), ("sort", dict(PDSC_SEED_SORT="1"))):
+        path = tmp_path / f"seeds_{tag}.npz"
         code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
                f"import test_gpu_seed_sort as t; t._dump({str(path)!r})"
-        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PDSC_SEED_SORT=knob), check=True,
-                       timeout=240)
-        res[knob] = np.load(path)
-    for k in res["0"].files:
-        assert np.array_equal(res["0"][k], res["1"][k]), k
+        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), check=True, timeout=240)
+        res[tag] = np.load(path)
+    for k in res["full"].files:
+        assert np.array_equal(res["full"][k], res["sort"][k]), k
