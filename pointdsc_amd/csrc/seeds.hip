@@ -20,7 +20,7 @@ namespace pdsc {
 // 1024-point LDS tiles (one tile for N <= 1024: one global-load round trip);
 // its 256 / SQ slices take disjoint parts of each tile, and the partial
 // results meet in LDS.  SQ = 64 for batches; SQ = 16 when the batch has fewer
-// than 512 row blocks of 64 (a single N = 1000 pair: 63 workgroups instead of
+// than 1024 row blocks of 64 (a single N = 1000 pair: 63 workgroups instead of
 // 16, each thread 64 compares instead of 256).
 constexpr int SEED_TILE = 1024;
 
@@ -239,7 +239,16 @@ __global__ __launch_bounds__(SORT_NT) void local_max_sort_kernel(const float *__
     lm[(size_t)b * Nstr + (int)(unsigned)skeys[q]] = viol ? 0.0f : 1.0f;
 }
 
-static bool seed_small(int B, int N) { return (long)B * ((N + 63) / 64) < 512; }
+// The 16-row kernels below 1024 blocks of 64 rows (r04: 8 x 5000, 632 blocks:
+// seed_rank 49 vs 61 us at 4x the waves, local_max equal; 128 x 1000 keeps 64).
+// A/B knob PDSC_SEED_BLOCKS (measurement only) moves the bound.
+static bool seed_small(int B, int N) {
+    static const long lim = [] {
+        const char *e = getenv("PDSC_SEED_BLOCKS");
+        return e ? atol(e) : 1024L;
+    }();
+    return (long)B * ((N + 63) / 64) < lim;
+}
 
 // The sorted forms are opt-in (A/B knob PDSC_SEED_SORT=1, measurement only):
 // r04 measured them slower than the compare kernels at every bench shape --

@@ -1,6 +1,7 @@
 """A/B timing of the batched testing forward (diagnostic): ms per forward for a
 few (B, N) shapes in THIS process (plan knobs such as PDSC_OVERLAP come from
-the environment).  Usage: python tools/forward_ab.py [reps]"""
+the environment; AB_SHAPES="8x5000,1x1000" picks the shapes).
+Usage: python tools/forward_ab.py [reps]"""
 import os
 import sys
 import time
@@ -22,7 +23,10 @@ def main():
     m.load_state_dict({k: torch.from_numpy(v) for k, v in trained_state_dict("3dmatch", 12, *BENCH_CLS).items()})
     m = m.to(dev).eval()
     out = []
-    for B, N in [(128, 1000), (8, 5000), (1, 1000)]:
+    shapes = [(128, 1000), (8, 5000), (1, 1000)]
+    if os.environ.get("AB_SHAPES"):
+        shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["AB_SHAPES"].split(",")]
+    for B, N in shapes:
         d = synthetic_batch(B, N, seed=7)
         c, s, t = (torch.from_numpy(d[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
         plan = kernels.ForwardPlan(m.pdsc_config(), m.packed_weights(), B, N, dev)
