@@ -695,13 +695,37 @@ template <int PTT> constexpr size_t pw_lds() { return (size_t)(2 * PTT * S132) *
 // PointCN_l (Xin -> Xout) then Q/K/V_l (Xout -> the attention's input layouts);
 // Xout rows -> feat.  Q, K, V point at the pair's buffers: the fp16 hi/lo split
 // layouts (H3) or fp32 [Npad][CH] rows (F32, same bytes).
+// only = 0 / 1 / 2 (H3): this workgroup writes Q / K / V alone (feat only with
+// Q), as pcn_qkv8's `only` (pw_first_kernel's z dimension).
 template <int PTT, bool F32>
 PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                       float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                      _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane) {
+                      _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane,
+                      int only = -1) {
     // four 128 -> 128 products with the same wave -> output-tile map (ct = wave):
     // each one's weight panel is fetched while the previous one computes
     WPanel<CH, F32> pa, pb;
+    if constexpr (!F32) {
+        if (only >= 0) {  // workgroup-uniform
+            load_wpanel<CH, CH, F32>(pk, d.pcn, wave, lane, pa);
+            load_wpanel<CH, CH, F32>(pk, only == 0 ? d.q : (only == 1 ? d.k : d.v), wave, lane, pb);
+            asm volatile("" ::: "memory");
+            dense_tile_w<CH, CH, EPI_BN_RELU, PTT / 32, F32>(Xin, S132, pa, pk, d.pcn, 0, wave, Xout, S132, nullptr,
+                                                             lane);
+            __syncthreads();  // Xout complete; Xin is dead (it now holds the split copy of Xout)
+            char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
+            split_tile<PTT>(Xout, S132, Xs, tid);
+            if (only == 0) store_rows<PTT>(Xout, S132, feat, p0, PTT, tid);
+            __syncthreads();
+            if (only == 0)
+                dense_split<SPLIT_Q, PTT / 32>(Xs, pb, pk, d.q, wave, Q, p0, lane);
+            else if (only == 1)
+                dense_split<SPLIT_K, PTT / 32>(Xs, pb, pk, d.k, wave, K, p0, lane);
+            else
+                dense_split<SPLIT_V, PTT / 32>(Xs, pb, pk, d.v, wave, V, p0, lane, Xout, vexp);  // Xout is dead
+            return;
+        }
+    }
     load_wpanel<CH, CH, F32>(pk, d.pcn, wave, lane, pa);
     load_wpanel<CH, CH, F32>(pk, d.q, wave, lane, pb);
     asm volatile("" ::: "memory");
@@ -741,15 +765,41 @@ PDSC_DEV void pcn_qkv(const float *Xin, float *Xout, const float *__restrict__ p
 // pcn_qkv for 8-wave workgroups (H3, 32-point tiles; small batches): PointCN on
 // waves 0-3, then Q (waves 0-3) and K (waves 4-7) at once, then V (waves 0-3).
 // Every output tile is the same dense_tile_w / dense_split code as the 4-wave
-// form, so the same bits.
+// form, so the same bits.  only = 0 / 1 / 2: this workgroup writes Q / K / V
+// alone (and feat only for Q): three workgroups per point tile share the
+// projections (pw_mid_kernel's z dimension), each streaming 4 of the chain's
+// 7 weight panels instead of all 7 -- the single pair's chain is bound by
+// each CU streaming its panels.
 template <int PTT>
 PDSC_DEV void pcn_qkv8(const float *Xin, float *Xout, const float *__restrict__ pk, const PwDense4 &d,
                        float *__restrict__ feat, _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                       _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane) {
+                       _Float16 *__restrict__ V, float *__restrict__ vexp, int p0, int tid, int wave, int lane,
+                       int only = -1) {
     static_assert(PTT == 32, "8-wave chain: 32-point tiles");
     const int w4 = wave & 3;
     const bool lo = wave < 4;
     WPanel<CH, false> pa, pb;
+    if (only >= 0) {  // workgroup-uniform
+        if (lo) {
+            load_wpanel<CH, CH, false>(pk, d.pcn, w4, lane, pa);
+            load_wpanel<CH, CH, false>(pk, only == 0 ? d.q : (only == 1 ? d.k : d.v), w4, lane, pb);
+        }
+        asm volatile("" ::: "memory");
+        if (lo) dense_tile_w<CH, CH, EPI_BN_RELU, 1, false>(Xin, S132, pa, pk, d.pcn, 0, w4, Xout, S132, nullptr, lane);
+        __syncthreads();  // Xout complete; Xin is dead (it now holds the split copy of Xout)
+        char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
+        split_tile<PTT, 512>(Xout, S132, Xs, tid);
+        if (only == 0) store_rows<PTT, 512>(Xout, S132, feat, p0, PTT, tid);
+        __syncthreads();
+        if (only == 0) {
+            if (lo) dense_split<SPLIT_Q, 1>(Xs, pb, pk, d.q, w4, Q, p0, lane);
+        } else if (only == 1) {
+            if (lo) dense_split<SPLIT_K, 1>(Xs, pb, pk, d.k, w4, K, p0, lane);
+        } else {
+            dense_split<SPLIT_V, 1>(Xs, pb, pk, d.v, w4, V, p0, lane, Xout, vexp, lo);  // Xout is dead
+        }
+        return;
+    }
     if (lo) {
         load_wpanel<CH, CH, false>(pk, d.pcn, w4, lane, pa);
         load_wpanel<CH, CH, false>(pk, d.q, w4, lane, pb);
@@ -822,7 +872,7 @@ __global__ __launch_bounds__(256, 2) void pw_first_kernel(const float *__restric
     }
     __syncthreads();
     pcn_qkv<PTT, F32>(XA, XB, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
+                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane, gridDim.z == 3 ? (int)blockIdx.z : -1);
 }
 
 // Combine the split partials of rows p0..p0+63 into X (stride S132); 4 threads per row.
@@ -882,7 +932,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(cons
     message_resid<PTT, F32, NWV>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
     if constexpr (NWV == 8)
         pcn_qkv8<PTT>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
+                      vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane, gridDim.z == 3 ? (int)blockIdx.z : -1);
     else
         pcn_qkv<PTT, F32>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                           vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane);
@@ -1747,6 +1797,17 @@ static bool pw_waves8(int B, int Npad) {
     return !off && (long)B * (Npad / 32) <= 256;
 }
 
+// 8-wave pw_mid with Q, K and V in three workgroups per point tile (pcn_qkv8's
+// `only`) while that stays within one workgroup per CU.  A/B knob
+// PDSC_PW_QKV_SPLIT=0 (measurement only; the same bits either way).
+static bool pw_qkv_split(int B, int Npad) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_PW_QKV_SPLIT");
+        return e && e[0] == '0';
+    }();
+    return !off && 3L * B * (Npad / 32) <= 256;
+}
+
 // One launch of pointwise kernel K<PTT, F32> with PTT and F32 picked at run time.
 #define PW_LAUNCH(K, rows, ...)                                                                         \
     do {                                                                                                \
@@ -1775,6 +1836,12 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
                            V, vexp, rg.nv);
         return hipGetLastError();
     }
+    if (!f32 && small_tiles(B, Npad) && pw_qkv_split(B, Npad)) {  // Q / K / V in three workgroups per tile
+        hipLaunchKernelGGL((pw_first_kernel<32, false>), dim3(Npad / 32, B, 3), dim3(256), pw_lds<32>(), s, packed,
+                           lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K, V, vexp,
+                           rg.nv);
+        return hipGetLastError();
+    }
     PW_LAUNCH(pw_first_kernel, Npad, packed, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad,
               feat, Q, K, V, vexp, rg.nv);
     return hipGetLastError();
@@ -1792,7 +1859,8 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
         return hipGetLastError();
     }
     if (!f32 && pw_waves8(B, Npad)) {
-        hipLaunchKernelGGL((pw_mid_kernel<32, false, 8>), dim3(Npad / 32, B), dim3(512), pw_lds<32>(), s, packed,
+        hipLaunchKernelGGL((pw_mid_kernel<32, false, 8>), dim3(Npad / 32, B, pw_qkv_split(B, Npad) ? 3 : 1), dim3(512),
+                           pw_lds<32>(), s, packed,
                            msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, Q,
                            K, V, vexp);
         return hipGetLastError();

@@ -419,6 +419,27 @@ def test_pw_waves8_bit_identical(gpu_device, tmp_path):
             assert np.array_equal(v, ref[k]), (B, N, k)
 
 
+def test_pw_qkv_split_bit_identical(gpu_device, tmp_path):
+    """Single pairs and 2-pair batches run the 8-wave pw_mid as three workgroups
+    per point tile, one per Q / K / V projection (pcn_qkv8's `only`): the same
+    bits as one workgroup writing all three (a child process with
+    PDSC_PW_QKV_SPLIT=0), encoder and forward, including a padded tail."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for B, N in ((1, 1000), (2, 777), (1, 2500)):
+        ours = _fusion_outputs(gpu_device, B, N)
+        out = tmp_path / f"qkv1_{B}_{N}.npz"
+        env = dict(os.environ, PDSC_PW_QKV_SPLIT="0")
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = np.load(out)
+        for k, v in ours.items():
+            assert np.array_equal(v, ref[k]), (B, N, k)
+
+
 def test_graph_replay_equals_eager(gpu_device):
     """ForwardPlan.capture(): a HIP-graph replay of the forward gives the eager
     result bitwise, and picks up new contents of the same input buffers; the
