@@ -844,11 +844,18 @@ hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int 
 constexpr int HSUM = 15;  // H[9], cA[3], cB[3]
 constexpr int HS = 8;     // seeds per count_inliers workgroup
 
+PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[3], float *T);
+
+// SOLVE (small batches, kabsch_small): lane 0 of the seed's wave also finishes
+// the Kabsch solve (kabsch_finish on the same 15 sums kabsch_solve_kernel would
+// read back: the same bits) and writes trans -- one launch instead of two.
+template <bool SOLVE>
 __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restrict__ src,
                                                           const float *__restrict__ tgt,
                                                           const int *__restrict__ knn,
                                                           const float *__restrict__ weights, int N,
-                                                          int S, int k, float *__restrict__ sums, Ragged rg) {
+                                                          int S, int k, float *__restrict__ sums, Ragged rg,
+                                                          float *__restrict__ trans) {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
     const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (s >= rg.s(b, S)) return;  // (N, S: the strides; knn entries lie below this pair's count)
@@ -871,13 +878,25 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
     const float am[3] = {ax - cA0, ay - cA1, az - cA2};
     const float bm[3] = {bx - cB0, by - cB1, bz - cB2};
     float out = 0.0f;  // lane e < 15 keeps sums[e]
+    float Hs[9];       // (every lane holds every wave sum)
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int jj = 0; jj < 3; ++jj) {
             const float h = wave_sum((am[i] * w) * bm[jj]);  // H = Am^T diag(w) Bm (:33)
+            Hs[3 * i + jj] = h;
             if (lane == 3 * i + jj) out = h;
         }
+    if constexpr (SOLVE) {
+        if (lane == 0) {
+            const float cA[3] = {cA0, cA1, cA2}, cB[3] = {cB0, cB1, cB2};
+            float T[16];
+            kabsch_finish(Hs, cA, cB, T);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) trans[((size_t)b * S + s) * 16 + e] = T[e];
+        }
+        return;
+    }
     if (lane == 9) out = cA0;
     if (lane == 10) out = cA1;
     if (lane == 11) out = cA2;
@@ -963,14 +982,31 @@ __global__ __launch_bounds__(256) void count_inliers_kernel(const float *__restr
     if (tid < ns) counts[(size_t)b * S + s0 + tid] = wc[0][tid] + wc[1][tid] + wc[2][tid] + wc[3][tid];
 }
 
+// One solve per seed wave (kabsch_sums_kernel<true>) while the batch has at
+// most 1024 seeds (a single pair: 100); past that the solve kernel's 64 seeds
+// per wave keep the fp64 work off a lane-per-wave schedule.  A/B knob
+// PDSC_KABSCH_FUSED=0 (measurement only; the same bits either way).
+static bool kabsch_small(int n) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_KABSCH_FUSED");
+        return e && e[0] == '0';
+    }();
+    return !off && n <= 1024;
+}
+
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
                              float *sums, hipStream_t s, Ragged rg) {
     const int wpb = seed_wpb(B, S);
-    hipLaunchKernelGGL(kabsch_sums_kernel, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn, weights,
-                       N, S, k, sums, rg);
     const int n = B * S;
-    hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, S, seed_trans, rg);
+    if (kabsch_small(n)) {
+        hipLaunchKernelGGL(kabsch_sums_kernel<true>, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn,
+                           weights, N, S, k, sums, rg, seed_trans);
+    } else {
+        hipLaunchKernelGGL(kabsch_sums_kernel<false>, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn,
+                           weights, N, S, k, sums, rg, seed_trans);
+        hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, S, seed_trans, rg);
+    }
     hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
                        seed_trans, N, S, sqrt_ge_threshold(tau), counts, rg);
     return hipGetLastError();

@@ -440,6 +440,27 @@ def test_pw_qkv_split_bit_identical(gpu_device, tmp_path):
             assert np.array_equal(v, ref[k]), (B, N, k)
 
 
+def test_kabsch_fused_bit_identical(gpu_device, tmp_path):
+    """Batches of <= 1024 seeds finish each seed's Kabsch solve in the wave that
+    summed it (kabsch_sums_kernel<true>): the same bits as the separate solve
+    kernel (a child process with PDSC_KABSCH_FUSED=0), a single pair and a
+    4-pair batch."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for B, N in ((1, 1000), (4, 2000)):
+        ours = _fusion_outputs(gpu_device, B, N)
+        out = tmp_path / f"kabsch2_{B}_{N}.npz"
+        env = dict(os.environ, PDSC_KABSCH_FUSED="0")
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_parity as t; t._dump_fusion_outputs({str(out)!r}, {B}, {N})"
+        subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+        ref = np.load(out)
+        for k, v in ours.items():
+            assert np.array_equal(v, ref[k]), (B, N, k)
+
+
 def test_graph_replay_equals_eager(gpu_device):
     """ForwardPlan.capture(): a HIP-graph replay of the forward gives the eager
     result bitwise, and picks up new contents of the same input buffers; the
