@@ -377,13 +377,16 @@ def main():
             flops = P * (4.0 * N * N * 128 + 2.0 * 86016 * N)
             kname, kdesc, n_launch = "attn_pw2_kernel<1>", "attn_pw2_kernel (attention_l + pointwise chain_l, packed M)", 11
         elif fused.value == 2:
+            # the split grid (attention_w64_kernel) or, where one round of one workgroup per CU
+            # beats it, the stream-K form (attention_w64_sk_kernel, always 256 workgroups): the
+            # committed profile does not record which batch shape a stream-K row is, so no lookup
             flops = P * 4.0 * N * N * 128
-            kname, kdesc, n_launch = "attention_w64_kernel", "attention_w64_kernel<xcd> (64-query waves, fragment-ordered M)", 12
+            kname, kdesc, n_launch = None, "attention_w64 (64-query waves, fragment-ordered M; split grid or stream-K)", 12
         else:
             flops = P * 4.0 * N * N * 128
             kname, kdesc, n_launch = "attention_h3_kernel<4>", "attention_h3_kernel<4,xcd>", 12
         achieved = flops / (att_ms * 1e-3) / 1e12
-        att_prof = profiled(kname, grid)
+        att_prof = profiled(kname, grid) if kname else None
         roofline = {"kernel": kdesc, "bound": "mfma",
                     "achieved": round(achieved, 3), "peak": round(PEAK_H3_TFLOPS, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_H3_TFLOPS, 4),
