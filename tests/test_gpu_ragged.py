@@ -166,3 +166,25 @@ def test_forward_list_small_pairs(gpu_device):
         if n <= 40:
             assert torch.equal(r["final_trans"], res[b]["final_trans"]), b
         np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
+
+
+def test_ragged_w64_extra_split_slots(gpu_device):
+    """24 pairs up to N = 1500 take the 64-query-wave split plan with 3 partial
+    slots per query block (the stream-K count a uniform batch of this shape
+    would use); a ragged batch runs the split grid, whose one key split leaves
+    slots 1 and 2 as empty splits (m = -inf, skipped by the combine).  Against
+    per-pair ``forward`` calls: labels bitwise, poses within 2e-4."""
+    import ctypes
+    from pointdsc_amd import _lib
+    m, _ = _model(gpu_device)
+    sizes = [1500 - 17 * i for i in range(24)]
+    plan, npad, ns = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(24, 1500, 0, ctypes.byref(plan)), "encoder_plan")
+    _lib.check(_lib.load().pdsc_attention_layout(24, 1500, 0, ctypes.byref(npad), ctypes.byref(ns)), "layout")
+    assert plan.value == 2 and ns.value == 3, (plan.value, ns.value)
+    ds = _datas(_pairs(sizes, seed=91), gpu_device)
+    res = m.forward_list(ds)
+    for b in range(0, 24, 3):
+        r = m(dict(ds[b], testing=True))
+        assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
+        np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
