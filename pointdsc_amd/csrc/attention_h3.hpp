@@ -334,7 +334,13 @@ PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
 // ring (attention_h3_lds_bytes), free again when this returns.
 // PACKED: M in the symmetric-packed tile layout (pdsc_internal.hpp); else dense [N][N].
 // vexp: [B][Npad/32] V-tile exponents (see above).
-template <int NW, bool PACKED>
+// EARLY (the split-K kernel on splits of >= 3 tiles, launch_attention): the
+// first two tiles' LDS-DMA and the first tile's M issued with the Q loads, ahead
+// of the one wait before the loop, and each later tile's M issued one tile
+// ahead.  Measured (A/B, one box): 4 x 5000 forward 2.405 vs 2.460 ms; on the
+// single pair's 2-tile splits 0.419 vs 0.417 ms, so those keep the plain loop.
+// The same arithmetic on the same operands: bit-identical either way.
+template <int NW, bool PACKED, bool EARLY = false>
 PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks,
                                 const _Float16 *__restrict__ Vs, const float *__restrict__ vexp,
                                 const float *__restrict__ M, const AttnGridH3 &g, const AttnBlock &blk, char *h3smem,
@@ -589,7 +595,14 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // or at the end of the previous tile: no faster, and the compiler copies
     // asm-loaded registers before the wait.  DESIGN.md section 7.)
     auto slot_base = [&](int st) { return h3smem + ((st - st0) % H3_NSLOT) * (H3_KTB + H3_VTB); };
-    if (st0 < st1) stage(st0, 0);
+    float mvA[16], evA;  // EARLY: the next tile's M, loaded a tile ahead
+    if (st0 < st1) {
+        stage(st0, 0);
+        if constexpr (EARLY) {
+            load_m(st0 * H3_TILE, mvA, evA);
+            if (st0 + 1 < st1) stage(st0 + 1, 1);
+        }
+    }
     sync();
     for (int st = st0; st < st1; ++st) {
         float mv[16], ev;
@@ -597,8 +610,18 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         const int si = 1 + 6 * min(st - st0, 23);
         st_si = si;
         ATT_STAMP(stp, si);
-        load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
-        if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
+        if constexpr (EARLY) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mv[r] = mvA[r];
+            ev = evA;
+            if (st + 1 < st1) load_m((st + 1) * H3_TILE, mvA, evA);
+            // tile st0 + 1 went out before the loop; tile st + 1's slot held tile
+            // st - 1, released by the barrier that ended iteration st - 1
+            if (st > st0 && st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
+        } else {
+            load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
+            if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
+        }
         // padding waves (q0 >= Npad) compute on clamped operands and store nothing
         qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl, st == st0);
         ATT_STAMP(stp, si + 3);
@@ -610,7 +633,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     l_run = halves_sum(l_run);
 }
 
-template <int NW, bool XCD, bool PACKED>
+template <int NW, bool XCD, bool PACKED, bool EARLY = false>
 __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
@@ -630,7 +653,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
 #endif
     f32x16 O[4];
     float m_run, l_run;
-    attention_h3_core<NW, PACKED>(Qs, Ks, Vs, vexp, M, g, blk, h3smem, wave, lane, O, m_run, l_run);
+    attention_h3_core<NW, PACKED, EARLY>(Qs, Ks, Vs, vexp, M, g, blk, h3smem, wave, lane, O, m_run, l_run);
     ATT_STAMP(stp, 161);
     ATT_RSTAMP(stp, 185);
     if (q0 >= Npad) return;

@@ -227,12 +227,21 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     g.nv = rg.nv;
     g.po = rg.po;
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
-    if (m_packed)
-        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), dim3(g.B * g.nqb * g.nsplit),
-                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, vexp, M, g, opart, ml);
+    const dim3 grid(g.B * g.nqb * g.nsplit), block(ATT_NW * 64);
+    const size_t lds = attention_h3_lds_bytes<ATT_NW>();
+    if (g.sps >= 3) {  // long splits: the early-issue loop (attention_h3_core's EARLY)
+        if (m_packed)
+            hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g,
+                               opart, ml);
+        else
+            hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false, true>), grid, block, lds, s, qs, ks, vs, vexp, M,
+                               g, opart, ml);
+    } else if (m_packed)
+        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart,
+                           ml);
     else
-        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), dim3(g.B * g.nqb * g.nsplit),
-                           dim3(ATT_NW * 64), attention_h3_lds_bytes<ATT_NW>(), s, qs, ks, vs, vexp, M, g, opart, ml);
+        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart,
+                           ml);
     return hipGetLastError();
 }
 
