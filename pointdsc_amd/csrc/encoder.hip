@@ -1041,6 +1041,13 @@ __global__ __launch_bounds__(256, 2) void pw_last_kernel(
 #ifndef PW2_WAVES
 #define PW2_WAVES 4
 #endif
+// The fused kernels' attention with attention_h3_core's early-issue loop
+// (measured, one box: 128 x 1000 forward 3.802 vs 3.831 ms over three A/B
+// pairs, attn_pw2 290.3 vs 291.7 us; ragged 4.51 vs 4.58 ms).  A/B build
+// -DPW2_EARLY=0: the plain loop.
+#ifndef PW2_EARLY
+#define PW2_EARLY 1
+#endif
 constexpr int PW2_W = PW2_WAVES;                      // waves per workgroup (32 points each)
 constexpr int PW2_OCC = PW2_W >= 8 ? 1 : 2;           // workgroups per CU (<= 256 VGPRs: 2 waves per SIMD)
 // 16 two-plane blocks = 32 KiB chunks (r04, A/B: -0.7 % per step at 128 x 1000
@@ -1523,7 +1530,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
 #endif
     f32x16 O[4];
     float m_run, l_run;
-    attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
+    attention_h3_core<PW2_W, PACKED, PW2_EARLY>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
     ATT_STAMP(stp, 170);
     // the K/V ring is free (the core ends on a barrier): weight chunks 0, 1 and the coefficients
     W2Pipe P{w2smem, 0};
@@ -1679,7 +1686,7 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_last_kernel(
     const bool active = blk.qb * PW2_PTS + wave * 32 < Npad;  // wave-uniform
     f32x16 O[4];
     float m_run, l_run;
-    attention_h3_core<PW2_W, PACKED>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
+    attention_h3_core<PW2_W, PACKED, PW2_EARLY>(Qs, Ks, Vs, vexp_in, M, g, blk, w2smem, wave, lane, O, m_run, l_run);
     W2Pipe P{w2smem, 0};
     float *cf = reinterpret_cast<float *>(w2smem + PW2_NSLOT * PW2_SLOT);
     for (int c = 0; c < PW2_NSLOT; ++c) w2_stage(pk, S, c, P.slot(c), wave, lane);
