@@ -528,9 +528,28 @@ def main():
         e_ms = event_time(lambda: plan1.run(c1, s1, t1), 20, stream)
         plan1.capture(c1, s1, t1)
         g_ms = event_time(lambda: plan1.run(c1, s1, t1), 50, stream)
-        single = {"num_corr": N, "eager_ms": round(e_ms, 4), "graph_ms": round(g_ms, 4),
-                  "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1)}
         del plan1
+        # the drop-in call as the reference's drivers make it (evaluation/test_3DMatch.py:52-53,
+        # demo_registration.py:117): model(data) per pair at bs = 1, host wall time of the whole
+        # call -- argument checks, packed-weight change check, workspace, ~48 launches and the
+        # synchronising fp16 range-guard read -- one call after the other
+        data1 = {"corr_pos": c1, "src_keypts": s1, "tgt_keypts": t1, "testing": True}
+        for _ in range(5):
+            model(data1)
+        torch.cuda.synchronize(dev)
+        packs0, walls = model.pack_count, []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            model(data1)
+            walls.append((time.perf_counter() - t0) * 1e3)
+        single = {"num_corr": N, "eager_ms": round(e_ms, 4), "graph_ms": round(g_ms, 4),
+                  "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1),
+                  "drop_in_ms": round(float(np.mean(walls)), 4), "drop_in_median_ms": round(float(np.median(walls)), 4),
+                  "drop_in_over_eager": round(float(np.mean(walls)) / e_ms, 3),
+                  "drop_in_repacks": model.pack_count - packs0,
+                  "drop_in_note": "PointDSC.forward({'testing': True, ...}) at bs = 1, host wall per call over 50 "
+                                  "calls (range-guard read included); eager_ms / graph_ms: device time of "
+                                  "ForwardPlan.run by HIP events"}
 
         # ---- a ragged batch (pdsc_forward_testing_ragged): P pairs of N_b ~ U[0.7 N, 1.3 N],
         # the evaluation loop's mixed sizes in one call (datasets/ThreeDMatch.py:268-290)

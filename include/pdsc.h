@@ -154,9 +154,14 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
                            int32_t B, int32_t N, int32_t C, int32_t precision, float *msg, void *workspace,
                            size_t workspace_bytes, pdsc_stream_t stream);
 
-/* The encoder's attention geometry for (B, N): padded rows per pair and the
- * number of key splits (partials opart [B,nsplit,Npad,C], ml [B,nsplit,Npad,2]
- * live in the encoder workspace).                                           */
+/* The TESTING / TRAINING FORWARD's attention geometry for (B, N): padded rows
+ * per pair and the number of key splits (partials opart [B,nsplit,Npad,C],
+ * ml [B,nsplit,Npad,2] in the forward workspace).  Both this query and
+ * pdsc_encoder_plan describe pdsc_forward_testing(_ragged/_debug) and
+ * pdsc_forward_training only: the standalone pdsc_encoder_f32 and
+ * pdsc_attention_f32 take a dense M and always run the h3 split-K plan
+ * (plan 0 or 1, never 2), whose split count may differ from the one
+ * reported here for shapes where the forward picks plan 2.                  */
 int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *Npad, int32_t *nsplit);
 
 /* The encoder's launch plan for (B, N, precision) (no reference counterpart):

@@ -24,12 +24,32 @@ inside the kernels.
 """
 from __future__ import annotations
 
+import ctypes
 import warnings
 
 import torch
 import torch.nn as nn
+from torch.nn.modules import module as _nn_module
 
 from . import _lib, kernels
+
+# Bumped whenever ANY module registers (or replaces) a parameter, buffer or
+# sub-module -- e.g. ``model.encoder.layer0.weight = nn.Parameter(...)``: the
+# packed weights of every PointDSC are then rebuilt on its next forward.  (New
+# modules bump it while they are built; an evaluation loop builds none.)
+_REGISTRATION_EPOCH = [0]
+
+
+def _bump_epoch(*_):
+    _REGISTRATION_EPOCH[0] += 1
+
+
+_nn_module.register_module_parameter_registration_hook(_bump_epoch)
+_nn_module.register_module_buffer_registration_hook(_bump_epoch)
+_nn_module.register_module_module_registration_hook(_bump_epoch)
+
+# workspaces up to this size stay cached per stream between forwards
+_WS_CACHE_LIMIT = 256 << 20
 
 
 class NonLocalBlock(nn.Module):
@@ -116,41 +136,133 @@ class PointDSC(nn.Module):
     def pdsc_config(self, precision=None) -> _lib.PdscConfig:
         """Hyper-parameters as the C ABI's ``pdsc_config`` (read at call time,
         so attribute edits after construction are honoured like the reference)."""
-        return _lib.make_config(self.in_dim, self.num_layers, self.num_channels, self.num_iterations,
-                                self.k, self.ratio, self.inlier_threshold, self.nms_radius,
-                                precision or self.precision)
+        key = (self.in_dim, self.num_layers, self.num_channels, self.num_iterations, self.k, self.ratio,
+               self.inlier_threshold, self.nms_radius, precision or self.precision)
+        cache = self.__dict__.setdefault("_cfg_cache", {})
+        cfg = cache.get(key)
+        if cfg is None:
+            cfg = cache[key] = _lib.make_config(*key[:4], key[4], *key[5:])
+        return cfg
+
+    def invalidate_packing(self):
+        """Forget the packed weights (rebuilt on the next forward).  Needed only
+        after edits the change check cannot see: writes through ``.data`` (a
+        tensor with its own version counter) or to storage shared with another
+        tensor; in-place edits of the parameters/buffers themselves,
+        ``load_state_dict``, ``.to()/.cuda()`` and parameter replacement are
+        detected."""
+        self.__dict__["_pack"] = None
+
+    def _apply(self, fn, *args, **kwargs):  # .to() / .cuda() / .float() ...
+        self.invalidate_packing()
+        return super()._apply(fn, *args, **kwargs)
+
+    def load_state_dict(self, *args, **kwargs):
+        self.invalidate_packing()
+        return super().load_state_dict(*args, **kwargs)
+
+    def _packable(self, cfg):
+        """{state_dict key: tensor} the kernels' blob is packed from (pdsc_param_name order)."""
+        L = _lib.load()
+        names = [L.pdsc_param_name(ctypes.byref(cfg), i).decode() for i in range(L.pdsc_param_count(ctypes.byref(cfg)))]
+        named = dict(self.named_parameters())
+        named.update(self.named_buffers())
+        missing = [n for n in names if n not in named]
+        if missing:
+            raise KeyError(f"missing parameters {missing[:4]}")
+        return {n: named[n] for n in names}
+
+    def _flatten(self, tensors, device_only=True):
+        """Re-home the packed parameters/buffers as views of ONE flat device buffer:
+        views share their base's version counter, so any in-place edit of any of
+        them (optimizer steps under no_grad, ``copy_`` in ``load_state_dict``,
+        ``mul_``...) bumps ``flat._version`` -- the per-forward change check is one
+        integer compare instead of walking 358 tensors (1.4 ms per call).
+        Values, names, shapes and requires_grad are unchanged; the Parameter
+        objects are new ones (state_dict() keys and contents are the same)."""
+        ts = list(tensors.values())
+        dev = ts[0].device
+        if not all((t.is_cuda or not device_only) and t.device == dev and t.dtype == torch.float32 for t in ts):
+            return None  # pack_weights raises the precise error (CPU tensor, dtype)
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        off = 0
+        for name, t in tensors.items():
+            view = flat[off:off + t.numel()].view(t.shape)
+            off += t.numel()
+            owner, _, leaf = name.rpartition(".")
+            mod = self.get_submodule(owner) if owner else self
+            if leaf in mod._parameters:  # plain dict writes: no registration hook fires
+                mod._parameters[leaf] = nn.Parameter(view, requires_grad=t.requires_grad)
+            else:
+                mod._buffers[leaf] = view
+        return flat
 
     def packed_weights(self, precision=None) -> torch.Tensor:
-        """Kernel-layout weights, re-packed whenever a parameter/buffer changes
-        (one cached packing per precision)."""
+        """Kernel-layout weights (one cached packing per precision), re-packed
+        when a parameter/buffer changed since: checked per call by the flat
+        buffer's version counter and the module-registration epoch (see
+        ``_flatten``, ``invalidate_packing``)."""
         precision = precision or self.precision
-        named = dict(self.named_parameters())
-        named.update(dict(self.named_buffers()))
-        key = tuple((n, t.data_ptr(), t._version) for n, t in sorted(named.items()))
-        cache = self.__dict__.setdefault("_packed_by_precision", {})
-        if precision not in cache or cache[precision][0] != key:
-            cache[precision] = (key, kernels.pack_weights(self.pdsc_config(precision), named))
-        return cache[precision][1]
+        st = self.__dict__.get("_pack")
+        layout = (self.in_dim, self.num_layers, self.num_channels)
+        if st is None or st["epoch"] != _REGISTRATION_EPOCH[0] or st["layout"] != layout:
+            cfg = self.pdsc_config(precision)
+            tensors = self._packable(cfg)
+            flat = self._flatten(tensors)
+            if flat is not None:
+                tensors = self._packable(cfg)  # the views
+            st = self.__dict__["_pack"] = {"epoch": _REGISTRATION_EPOCH[0], "layout": layout, "flat": flat,
+                                           "version": None if flat is None else flat._version,
+                                           "tensors": tensors, "packed": {}}
+        elif st["flat"] is not None and st["flat"]._version != st["version"]:  # values edited in place
+            st["version"], st["packed"] = st["flat"]._version, {}
+        if precision not in st["packed"]:
+            st["packed"][precision] = kernels.pack_weights(self.pdsc_config(precision), st["tensors"])
+            self.__dict__["pack_count"] = self.__dict__.get("pack_count", 0) + 1
+        return st["packed"][precision]
+
+    def _workspace(self, cfg, B, N, device):
+        """The forward's workspace for (cfg, B, N) on the current stream, cached
+        per stream (stream order keeps consecutive forwards apart)."""
+        nb = _lib.load().pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
+        if nb == 0 or nb > _WS_CACHE_LIMIT:
+            return None  # forward_testing allocates (or reports the unsupported configuration)
+        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        cache = self.__dict__.setdefault("_ws_cache", {})
+        ws = cache.get(key)
+        if ws is None or ws.numel() < nb:
+            ws = cache[key] = torch.empty(nb, dtype=torch.uint8, device=device)
+        return ws
 
     def _range_guarded(self, run):
         """run(cfg, packed, idx) -> the outputs' tuple for the pairs idx (None: all).
         Pairs the fp16 range guard marks (kernels.RangeError; include/pdsc.h) are
         run again with exact fp32 contractions and spliced into the result, so a
-        forward never returns their NaN pose; in 'f32' the error propagates (its
-        marks are non-finite logits, e.g. from non-finite inputs)."""
+        forward never returns the 3xfp16 path's NaN pose for them.  A pair still
+        marked in exact fp32 (non-finite logits, e.g. from non-finite inputs;
+        also the 'f32' model's only marks) keeps the marked result -- NaN pose,
+        zero labels, as the reference's own arithmetic would give NaN -- with a
+        warning: the other pairs' results are returned either way."""
         try:
             return run(self.pdsc_config(), self.packed_weights(), None)
         except kernels.RangeError as e:
-            if self.precision == "f32":
-                raise
-            warnings.warn(f"pairs {e.pairs}: activations beyond fp16's range in the 3xfp16 path; "
+            out, bad = e.outputs, e.pairs
+        if self.precision != "f32":
+            warnings.warn(f"pairs {bad}: activations beyond fp16's range in the 3xfp16 path; "
                           f"recomputed with exact fp32 contractions", RuntimeWarning, stacklevel=3)
-            out, redo = e.outputs, run(self.pdsc_config("f32"), self.packed_weights("f32"), e.pairs)
-            idx = torch.tensor(e.pairs, device=out[0].device)
+            try:
+                redo, still = run(self.pdsc_config("f32"), self.packed_weights("f32"), bad), []
+            except kernels.RangeError as e2:
+                redo, still = e2.outputs, [bad[i] for i in e2.pairs]
+            idx = torch.tensor(bad, device=out[0].device)
             for t, r in zip(out, redo):
                 if t is not None:
                     t[idx] = r
-            return out
+            bad = still
+        if bad:
+            warnings.warn(f"pairs {bad}: non-finite logits in exact fp32 as well (non-finite inputs?); their "
+                          f"final_trans is NaN and final_labels 0", RuntimeWarning, stacklevel=3)
+        return out
 
     # --------------------------------------------------------------- forward
     def forward(self, data):
@@ -168,7 +280,8 @@ class PointDSC(nn.Module):
             return {"final_trans": trans, "final_labels": conf, "M": M}
         assert corr_pos.shape[0] == 1  # pick_seeds / post_refinement support bs = 1 only
         trans, labels = self._range_guarded(lambda cfg, pk, i: kernels.forward_testing(
-            cfg, pk, *_rows((corr_pos, src, tgt), i)))
+            cfg, pk, *_rows((corr_pos, src, tgt), i),
+            ws=self._workspace(cfg, 1, src.shape[1], src.device) if src.is_cuda and i is None else None))
         return {"final_trans": trans, "final_labels": labels, "M": None}
 
     def forward_list(self, datas):

@@ -134,6 +134,7 @@ int forward_m_layout(const Dims &d) {
 
 struct EncBufs {
     float *feat, *opart, *ml, *vexp, *vexp2;
+    float *feat2;            // the split path's second feat buffer (pw_mid reads one, writes the other), else null
     _Float16 *q, *k, *v;     // attention_h3 split layouts (hi + lo per element), or fp32 rows (F32)
     _Float16 *q2, *k2, *v2;  // the other Q/K/V set of the fused path (layers alternate), else null
     float *opart1, *ml1;     // the combined split (Dims::precombine), else null
@@ -153,6 +154,11 @@ EncBufs carve_encoder(Carve &c, const Dims &d) {
     e.ml1 = d.precombine ? c.take<float>((size_t)d.B * d.Npad * 2) : nullptr;
     e.q2 = e.k2 = e.v2 = nullptr;
     e.vexp2 = nullptr;
+    // pw_mid's three Q / K / V workgroups per point tile all read the layer's
+    // residual rows while one of them writes the new PointCN rows: the rows
+    // ping-pong between feat and feat2 so no workgroup overwrites what another
+    // still reads
+    e.feat2 = d.fuse ? nullptr : c.take<float>(rows);
     if (d.fuse) {
         e.q2 = c.take<_Float16>(2 * rows);
         e.k2 = c.take<_Float16>(2 * rows);
@@ -186,6 +192,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                                     normed_s, conf, s, rg));
         return PDSC_OK;
     }
+    float *feat = e.feat, *feat_alt = e.feat2;
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
@@ -200,12 +207,14 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
             mlp = e.ml1;
             ns = 1;
         }
-        if (l + 1 < lay.L)
-            HIPCHK(launch_pw_mid(packed, lay, l, d.f32, op, mlp, ns, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp,
-                                 s));
-        else
-            HIPCHK(launch_pw_last(packed, lay, d.f32, op, mlp, ns, d.B, d.N, d.Npad, e.feat, feat_out, normed,
+        if (l + 1 < lay.L) {
+            HIPCHK(launch_pw_mid(packed, lay, l, d.f32, op, mlp, ns, d.B, d.N, d.Npad, feat, feat_alt, e.q, e.k, e.v,
+                                 e.vexp, s));
+            std::swap(feat, feat_alt);
+        } else {
+            HIPCHK(launch_pw_last(packed, lay, d.f32, op, mlp, ns, d.B, d.N, d.Npad, feat, feat_out, normed,
                                   d.f32 ? nullptr : normed_s, conf, s));
+        }
     }
     return PDSC_OK;
 }

@@ -922,13 +922,21 @@ template <int PTT, bool F32, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
                                                      const float *__restrict__ ml, int nsplit, int N,
-                                                     int Npad, float *__restrict__ feat,
+                                                     int Npad, const float *__restrict__ feat_in,
+                                                     float *__restrict__ feat,
                                                      _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
-                                                     _Float16 *__restrict__ V, float *__restrict__ vexp) {
+                                                     _Float16 *__restrict__ V, float *__restrict__ vexp,
+                                                     int diag_delay) {
+    // feat_in != feat: with gridDim.z == 3 the three workgroups of a point tile
+    // read feat_in's rows as fc6's residual while the z = 0 one writes feat
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float *XA = sm, *XB = sm + PTT * S132, *XC = XB;
     const int b = blockIdx.y, p0 = blockIdx.x * PTT;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    // diagnostic (PDSC_DIAG_QKV_DELAY, tests only): the K / V workgroups start
+    // late, after the Q one has stored its PointCN rows
+    if (diag_delay > 0 && blockIdx.z != 0)
+        for (int i = 0; i < diag_delay; ++i) __builtin_amdgcn_s_sleep(127);
     const size_t boff = (size_t)b * Npad * CH;
 #ifdef ATT_STAMPS
     unsigned long long *stp = att_stamp_ptr(wave);
@@ -938,7 +946,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(cons
     if (tid < 256) combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     ATT_STAMP(stp, 151);
-    message_resid<PTT, F32, NWV>(XA, XC, XB, pk, m, feat + boff + (size_t)p0 * CH, wave, lane);
+    message_resid<PTT, F32, NWV>(XA, XC, XB, pk, m, feat_in + boff + (size_t)p0 * CH, wave, lane);
     if constexpr (NWV == 8)
         pcn_qkv8<PTT>(XB, XA, pk, d, feat + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
                       vexp + (size_t)b * (Npad / 32), p0, tid, wave, lane, gridDim.z == 3 ? (int)blockIdx.z : -1);
@@ -1409,9 +1417,11 @@ PDSC_DEV void w2_coef_mid(float *cf, const float *__restrict__ pk, const PwMsg &
 // fc_message + residual + PointCN + QKV from the message fragments x (after the
 // combine); the pipeline is at fc0's first chunk.  featL, Q, K, V, vexp: the pair's.
 PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sched &S, const float *cf, const PwMsg &m,
-                           const PwDense4 &d, f16x8 *xh, f16x8 *xl, float *__restrict__ featL,
+                           const PwDense4 &d, f16x8 *xh, f16x8 *xl, const float *featL_in, float *featL,
                            _Float16 *__restrict__ Q, _Float16 *__restrict__ K, _Float16 *__restrict__ V,
                            float *__restrict__ vexp, int row, bool active, int wave, int lane) {
+    // featL_in: the residual rows; featL: where the PointCN rows go (each lane
+    // reads and writes only its own row, so the two may be one buffer)
     f32x16 a2[2], a4[4], res[4];
     f16x8 yh[8], yl[8];
     w2_layer<CH, CH2, true>(P, pk, S, xh, xl, a2, active, wave, lane);
@@ -1420,7 +1430,7 @@ PDSC_DEV void w2_mid_chain(W2Pipe &P, const float *__restrict__ pk, const W2Sche
     w2_layer<CH2, CH2, true>(P, pk, S, yh, yl, a2, active, wave, lane);
     if (active) {
         w2_epilogue<CH2, EPI_BN_RELU>(a2, pk[m.fc3.scale], cf + W2CoefMid::f3, nullptr, xh, xl, lane);
-        w2_load_row(featL, row, lane, res);  // the residual: lands during fc6's MFMAs
+        w2_load_row(featL_in, row, lane, res);  // the residual: lands during fc6's MFMAs
     }
     CH_STAMP(173);
     w2_layer<CH2, CH, true, 16>(P, pk, S, xh, xl, a4, active, wave, lane);
@@ -1488,7 +1498,8 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_first_kernel(const fl
 __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const float *__restrict__ pk, W2Sched S, PwMsg m,
                                                                PwDense4 d, const float *__restrict__ opart,
                                                                const float *__restrict__ ml, int nsplit, int N,
-                                                               int Npad, float *__restrict__ featL,
+                                                               int Npad, const float *__restrict__ featL_in,
+                                                               float *__restrict__ featL,
                                                                _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                                _Float16 *__restrict__ V, float *__restrict__ vexp) {
     PW2_PROLOGUE
@@ -1496,8 +1507,8 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const floa
     f16x8 xh[8], xl[8];
     if (active) w2_combine(opart, ml, b, nsplit, Npad, row, xh, xl, lane);
     __syncthreads();
-    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                 vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL_in + boff, featL + boff, Q + 2 * boff, K + 2 * boff,
+                 V + 2 * boff, vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
 }
 
 // attention_l + fc_message_l + residual + PointCN_{l+1} + QKV_{l+1} in ONE
@@ -1541,8 +1552,8 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     if (active) w2_msg_frags(O, l_run, xh, xl);  // msg = O / l
     __syncthreads();
     ATT_STAMP(stp, 171);
-    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, Q + 2 * boff, K + 2 * boff, V + 2 * boff,
-                 vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
+    w2_mid_chain(P, pk, S, cf, m, d, xh, xl, featL + boff, featL + boff, Q + 2 * boff, K + 2 * boff,
+                 V + 2 * boff, vexp + (size_t)b * (Npad / 32), row, active, wave, lane);
     ATT_STAMP(stp, 180);
     ATT_RSTAMP(stp, 189);
 }
@@ -1864,25 +1875,27 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
 }
 
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
-                         float *vexp, hipStream_t s) {
+                         const float *ml, int nsplit, int B, int N, int Npad, const float *feat_in, float *feat,
+                         void *q, void *k, void *v, float *vexp, hipStream_t s) {
+    const char *dd = getenv("PDSC_DIAG_QKV_DELAY");  // tests only: delay the split's K / V workgroups
+    const int delay = dd ? atoi(dd) : 0;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
         const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
         hipLaunchKernelGGL(pw2_mid_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
                            packed, S, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad,
-                           feat, Q, K, V, vexp);
+                           feat_in, feat, Q, K, V, vexp);
         return hipGetLastError();
     }
     if (!f32 && pw_waves8(B, Npad)) {
         hipLaunchKernelGGL((pw_mid_kernel<32, false, 8>), dim3(Npad / 32, B, pw_qkv_split(B, Npad) ? 3 : 1), dim3(512),
                            pw_lds<32>(), s, packed,
-                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat, Q,
-                           K, V, vexp);
+                           msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat_in,
+                           feat, Q, K, V, vexp, delay);
         return hipGetLastError();
     }
     PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,
-              N, Npad, feat, Q, K, V, vexp);
+              N, Npad, feat_in, feat, Q, K, V, vexp, 0);
     return hipGetLastError();
 }
 

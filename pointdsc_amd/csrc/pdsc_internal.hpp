@@ -228,9 +228,12 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
 // batches: combine16's per-thread load chain is the pointwise launch's latency).
 hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int Npad, int nsplit, float *opart1,
                                float *ml1, hipStream_t s);
+// feat_in: the layer's rows (the residual); feat: where the new PointCN rows
+// go -- a different buffer (the Q / K / V workgroups of one point tile read
+// feat_in while one of them writes feat)
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
-                         const float *ml, int nsplit, int B, int N, int Npad, float *feat, void *q, void *k, void *v,
-                         float *vexp, hipStream_t s);
+                         const float *ml, int nsplit, int B, int N, int Npad, const float *feat_in, float *feat,
+                         void *q, void *k, void *v, float *vexp, hipStream_t s);
 hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, const float *opart,
                           const float *ml, int nsplit, int B, int N, int Npad, const float *feat,
                           float *feat_out, float *normed, _Float16 *normed_s, float *conf, hipStream_t s);

@@ -281,10 +281,14 @@ def _check_inputs(cfg, corr_pos, src, tgt):
                          f"src {tuple(src.shape)}, tgt {tuple(tgt.shape)} (expected [B,N,3])")
 
 
-def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False, check_range=True):
+def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False, check_range=True, ws=None):
     """Full testing forward for B pairs: (final_trans [B,4,4], final_labels [B,N])
     (+ (confidence [B,N], seeds [B,S]) when ``debug``).  check_range: read the
-    fp16 range guard's marks (synchronises) and raise RangeError if any."""
+    fp16 range guard's marks (synchronises the stream) and raise RangeError if
+    any; with check_range=False the call stays asynchronous and the caller reads
+    the marks itself (``range_flags(ws, B, device)``) before trusting a pose.
+    ws: a caller-kept uint8 device workspace of at least
+    pdsc_forward_workspace_bytes (else one is allocated per call)."""
     corr_pos, src, tgt = _dev(corr_pos, "corr_pos"), _dev(src, "src_keypts"), _dev(tgt, "tgt_keypts")
     B, N, _ = src.shape
     _check_inputs(cfg, corr_pos, src, tgt)
@@ -293,7 +297,8 @@ def forward_testing(cfg, packed, corr_pos, src, tgt, debug=False, check_range=Tr
     nb = L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), B, N)
     if nb == 0:
         raise RuntimeError(f"unsupported configuration: {L.pdsc_last_error().decode()}")
-    ws = _workspace(nb, dev)
+    if ws is None or ws.numel() < nb or ws.device != dev:
+        ws = _workspace(nb, dev)
     trans = torch.empty((B, 4, 4), dtype=torch.float32, device=dev)
     labels = torch.empty((B, N), dtype=torch.float32, device=dev)
     conf = seeds = None

@@ -440,6 +440,22 @@ def test_pw_qkv_split_bit_identical(gpu_device, tmp_path):
             assert np.array_equal(v, ref[k]), (B, N, k)
 
 
+def test_pw_qkv_split_delayed_readers(gpu_device, monkeypatch):
+    """The split pw_mid's K and V workgroups read the layer's residual rows that
+    the Q workgroup replaces with the new PointCN rows: the rows ping-pong
+    between two feat buffers, so delaying the K / V workgroups until the Q one
+    has stored (PDSC_DIAG_QKV_DELAY: s_sleep loops before their first load) must
+    leave every output bit unchanged.  Before the ping-pong this read the new
+    rows as the residual (wrong K / V)."""
+    for B, N in ((1, 1000), (2, 777)):
+        ref = _fusion_outputs(gpu_device, B, N)
+        monkeypatch.setenv("PDSC_DIAG_QKV_DELAY", "24")  # ~100 us: longer than the whole pw_mid launch
+        late = _fusion_outputs(gpu_device, B, N)
+        monkeypatch.delenv("PDSC_DIAG_QKV_DELAY")
+        for k, v in ref.items():
+            assert np.array_equal(v, late[k]), (B, N, k)
+
+
 def test_kabsch_fused_bit_identical(gpu_device, tmp_path):
     """Batches of <= 1024 seeds finish each seed's Kabsch solve in the wave that
     summed it (kabsch_sums_kernel<true>): the same bits as the separate solve

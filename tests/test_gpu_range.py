@@ -114,3 +114,74 @@ def test_training_forward_range_guard(gpu_device):
     with pytest.warns(RuntimeWarning):
         r = m({"corr_pos": corr, "src_keypts": src, "tgt_keypts": tgt})
     assert torch.isfinite(r["final_trans"]).all()
+
+
+def _plan2_child(path, sk):  # child process entry: the split-grid (PDSC_W64_SK=0) arm
+    import os
+    os.environ["PDSC_W64_SK"] = sk
+    from pointdsc_amd import kernels
+    dev = torch.device("cuda:0")
+    m = _model(dev, "h3")
+    corr, src, tgt = _batch(dev, B=8, N=5000)
+    try:
+        kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr, src, tgt)
+        pairs, T, L = [], None, None
+    except kernels.RangeError as e:
+        pairs, (T, L) = e.pairs, e.outputs
+    np.savez(path, pairs=np.array(pairs), T=T.cpu().numpy(), L=L.cpu().numpy())
+
+
+def test_range_guard_on_the_split_plan(gpu_device, tmp_path):
+    """The key-split plan (pdsc_encoder_plan 2: attention_w64 on fragment-ordered
+    M, stream-K by default and the split grid with PDSC_W64_SK=0), whose combine
+    skips a split whose running max stayed -inf (fmaxf ignores NaN): a scaled
+    pair among 8 x 5000 is still marked, its pose NaN and labels 0, every other
+    pair bitwise as without it, and the module splices the exact-fp32 rerun."""
+    import os
+    import subprocess
+    import sys
+    from pointdsc_amd import _lib, kernels
+    plan = ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(8, 5000, 0, ctypes.byref(plan)), "encoder_plan")
+    assert plan.value == 2
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device, B=8, N=5000)
+    corr0, _, _ = _batch(gpu_device, B=8, N=5000, bad=())
+    T0, L0 = kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr0, src, tgt)
+    here = os.path.dirname(os.path.abspath(__file__))
+    arms = {}
+    for sk in ("1", "0"):
+        out = tmp_path / f"plan2_sk{sk}.npz"
+        code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
+               f"import test_gpu_range as t; t._plan2_child({str(out)!r}, {sk!r})"
+        subprocess.run([sys.executable, "-c", code], check=True, timeout=240)
+        arms[sk] = np.load(out)
+    for sk, r in arms.items():
+        assert list(r["pairs"]) == [2], sk
+        assert np.isnan(r["T"][2]).all() and float(np.abs(r["L"][2]).sum()) == 0.0, sk
+    with pytest.raises(kernels.RangeError) as ei:
+        kernels.forward_testing(m.pdsc_config(), m.packed_weights(), corr, src, tgt)
+    T, L = ei.value.outputs
+    for b in (0, 1, 3, 4, 5, 6, 7):
+        assert torch.equal(T[b], T0[b]) and torch.equal(L[b], L0[b]), b
+    with pytest.warns(RuntimeWarning, match="fp16"):
+        Tm, Lm = m.forward_batched(corr, src, tgt)
+    assert torch.isfinite(Tm).all()
+    m32 = _model(gpu_device, "f32")
+    T32, L32 = m32.forward_batched(corr[2:3], src[2:3], tgt[2:3])
+    assert torch.equal(Tm[2], T32[0]) and torch.equal(Lm[2], L32[0])
+
+
+def test_nonfinite_input_keeps_other_pairs(gpu_device):
+    """A pair with a NaN coordinate is marked in both precisions: the module
+    returns every other pair's result (bitwise the clean batch's) and that
+    pair's NaN pose / zero labels with a warning, instead of raising."""
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device, bad=())
+    T0, L0 = m.forward_batched(corr, src, tgt)
+    corr[1, 5, 0] = float("nan")
+    with pytest.warns(RuntimeWarning, match="non-finite"):
+        T, L = m.forward_batched(corr, src, tgt)
+    assert torch.isnan(T[1]).all() and float(L[1].abs().sum()) == 0.0
+    for b in (0, 2, 3):
+        assert torch.equal(T[b], T0[b]) and torch.equal(L[b], L0[b]), b

@@ -122,3 +122,40 @@ def test_ragged_counts_validated_on_host():
     rc = lib.pdsc_forward_testing_ragged(ctypes.byref(cfg), dummy, dummy, dummy, dummy, 2, 1000, None, dummy,
                                          dummy, None, dummy, 1, None)
     assert rc == 1
+
+
+def test_flat_weight_views_track_edits():
+    """PointDSC re-homes the packed parameters/buffers as views of one flat
+    buffer (PointDSC._flatten; on the device in a forward, on the CPU here):
+    state_dict keys, values and requires_grad are unchanged, and every kind of
+    in-place edit -- an optimizer-style update under no_grad, load_state_dict's
+    copy_, a running statistic -- bumps the ONE version counter the per-forward
+    change check reads; replacing a Parameter bumps the registration epoch."""
+    import torch
+    import torch.nn as nn
+    from pointdsc_amd import PointDSC as mod
+    m = mod.PointDSC(num_layers=3)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    grads = {k: p.requires_grad for k, p in m.named_parameters()}
+    tensors = m._packable(m.pdsc_config())
+    flat = m._flatten(tensors, device_only=False)
+    assert flat is not None and flat.numel() == sum(t.numel() for t in tensors.values())
+    after = m.state_dict()
+    assert list(after) == list(before)
+    assert all(torch.equal(after[k], before[k]) for k in before)
+    assert {k: p.requires_grad for k, p in m.named_parameters()} == grads
+    views = m._packable(m.pdsc_config())
+    assert all(t.data_ptr() >= flat.data_ptr() for t in views.values())
+    v = flat._version
+    with torch.no_grad():
+        m.encoder.layer0.weight.mul_(2)
+    assert flat._version != v
+    v = flat._version
+    m.encoder.blocks["PointCN_layer_1"][1].running_var.add_(1)
+    assert flat._version != v
+    v = flat._version
+    m.load_state_dict(before)
+    assert flat._version != v and torch.equal(m.state_dict()["encoder.layer0.weight"], before["encoder.layer0.weight"])
+    e = mod._REGISTRATION_EPOCH[0]
+    m.classification[4].bias = nn.Parameter(torch.zeros(1))
+    assert mod._REGISTRATION_EPOCH[0] != e
