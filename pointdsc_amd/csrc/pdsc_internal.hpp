@@ -201,8 +201,13 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 // the split path's attention as attention_w64 (fragment-ordered M) for this shape?
 bool attention_w64(int B, int N, bool f32);
 int attention_nsplit(int B, int N, bool f32, bool w64 = false);
-// M's layouts: dense [B][N][N], symmetric-packed (mpack_*), fragment-ordered (mfrag_*)
-enum MLayout { M_DENSE = 0, M_PACKED = 1, M_FRAG = 2 };
+// M's layouts: dense [B][N][N], symmetric-packed (mpack_floats: the triangular
+// fragment order, mtri_block), fragment-ordered (mfrag_*); M_TRI_W64 is M_PACKED's
+// bytes for the attention_w64 plan
+enum MLayout { M_DENSE = 0, M_PACKED = 1, M_FRAG = 2, M_TRI_W64 = 3 };
+// the w64 plan's M: the triangular order (default) or the dense fragment order
+// (knob PDSC_W64_MTRI=0, measurement only)
+bool w64_mtri();
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
 // or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
 // M: dense [B][N][N], symmetric-packed [B][mpack_floats(N)] (H3) or fragment-ordered
