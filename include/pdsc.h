@@ -115,13 +115,11 @@ int32_t pdsc_pack_weights(const pdsc_config *cfg, const float *const *params_hos
  * src,tgt [B,N,3]; M [B,N,N].                                              */
 int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                         const float *sigma_d_dev, float *M, pdsc_stream_t stream);
-/* The forward's form of the same M (symmetric, stored once): for every pair of
- * 32-tiles a >= b (nt = ceil(N/32) per side) one contiguous 4 KiB block at
- * float offset (a*(a+1)/2 + b)*1024, in the lane order of the attention's
- * S^T accumulator: lane l (h = l/32, q = l%32) holds
- * M[32b + (r%4) + 8(r/4) + 4h][32a + q] at l*16 + r, r = 0..15; M[i][j] with
- * i/32 > j/32 is the same block's M[j][i].  Entries past N are 0.
- * Mp: B * pdsc_compat_packed_floats(N) floats (half the dense bytes).        */
+/* The forward's form of the same M: the upper triangle of 32 x 32 tiles, each
+ * a contiguous row-major 4 KiB block, tile (ti, tj), ti <= tj, at block index
+ * ti*nt - ti*(ti-1)/2 + (tj - ti), nt = ceil(N/32); M[i][j] for i > j is
+ * element (j%32, i%32) of tile (j/32, i/32); entries past N are 0.
+ * Mp: B * pdsc_compat_packed_floats(N) floats.                              */
 size_t pdsc_compat_packed_floats(int32_t N);
 int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                                const float *sigma_d_dev, float *Mp, pdsc_stream_t stream);

@@ -128,7 +128,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
 }
 
 int forward_m_layout(const Dims &d) {
-    if (d.w64) return w64_mtri() ? M_TRI_W64 : M_FRAG;
+    if (d.w64) return M_FRAG;
     return (!dense_m_requested() && !d.f32) ? M_PACKED : M_DENSE;
 }
 
@@ -172,8 +172,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                 int m_layout, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s, Ragged rg = {}) {
     const bool m_packed = m_layout == M_PACKED;
-    if ((m_layout == M_FRAG || m_layout == M_TRI_W64) != (d.w64 && !d.fuse))
-        return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
+    if ((m_layout == M_FRAG) != (d.w64 && !d.fuse)) return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg));
     if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
@@ -733,7 +732,7 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     const int mlay = forward_m_layout(d);
     if (mlay == M_FRAG)
         HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
-    else if (mlay == M_PACKED || mlay == M_TRI_W64)
+    else if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
@@ -814,7 +813,7 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     const int mlay = forward_m_layout(d);
     if (mlay == M_FRAG)
         HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s));
-    else if (mlay == M_PACKED || mlay == M_TRI_W64)
+    else if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));

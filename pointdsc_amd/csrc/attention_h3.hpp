@@ -415,38 +415,13 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // M[key][q] = M[q][key] (M symmetric) for this lane's 16 keys of tile key0
     auto load_m = [&](int key0, float (&mv)[16], float &ev) {
         if constexpr (PACKED) {
-            static_assert(MPACK_T == 32, "one packed tile per wave step");
-            const int kt = key0 / MPACK_T, qt = q0 / MPACK_T;
-#if PDSC_MTRI
-            // the triangular fragment order (pdsc_internal.hpp): block (qt, kt),
-            // kt <= qt, is this lane's 16 values contiguous (4 loads, 1 KiB per
-            // wave instruction); else block (kt, qt) transposed: register
-            // r' = (q & 3) + 4 (q >> 3) of lanes 32 ((q >> 2) & 1) + acc_row(r, h)
-            // (16 dword loads, four whole 64-B segments per wave instruction).
-            // Scalar branch (q0 is wave-uniform in an SGPR).
-            if (kt <= qt) {
-                const uint32_t vo = ((uint32_t)mtri_block(qt, kt) * (MPACK_T * MPACK_T) + 16u * lane) * 4;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x4 v4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rM, vo + 16 * g, 0, 0));
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[e];
-                }
-            } else {
-                const int hp = (l32 >> 2) & 1, rp = (l32 & 3) + 4 * (l32 >> 3);
-                const uint32_t vo =
-                    ((uint32_t)mtri_block(kt, qt) * (MPACK_T * MPACK_T) + (uint32_t)(16 * (32 * hp + 4 * h) + rp)) * 4;
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    mv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                          rM, vo + (uint32_t)((r & 3) + 8 * (r >> 2)) * 64, 0, 0));
-            }
-#else
             // the wave's 32 x 32 block IS one packed tile: (kt, qt) row-major when
             // kt <= qt (rows = keys: 16 loads, each 32 consecutive queries of a key
             // row), else tile (qt, kt) read transposed (rows = queries: the lane's
             // 16 keys are 4 runs of 4 in its query's row).  Scalar branch (q0 is
             // wave-uniform in an SGPR).
+            static_assert(MPACK_T == 32, "one packed tile per wave step");
+            const int kt = key0 / MPACK_T, qt = q0 / MPACK_T;
             const int kr = 4 * h, qr = l32;
             if (kt <= qt) {  // rows = keys
                 const uint32_t vo =
@@ -465,7 +440,6 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
                     for (int e = 0; e < 4; ++e) mv[4 * g + e] = v4[e];
                 }
             }
-#endif
         } else {
             const uint32_t vo = ((uint32_t)(key0 + 4 * h) * (uint32_t)g.N + (uint32_t)qq) * 4;
 #pragma unroll

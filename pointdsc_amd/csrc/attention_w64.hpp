@@ -43,18 +43,6 @@ constexpr int W64_NSLOT = 4;                 // K/V ring slots (V(t-1) is read i
 constexpr size_t W64_RING = (size_t)W64_NSLOT * (H3_KTB + H3_VTB);  // 128 KiB
 constexpr int W64_MAXT = 1024;                                       // V-tile exponents in LDS (N <= 32767)
 constexpr size_t W64_LDS = W64_RING + W64_MAXT * sizeof(float);
-// TRI (M in the triangular fragment order, pdsc_internal.hpp mtri_block): K in
-// a 3-slot ring (K(t-1) is dead once QK_B(t-1) ran, before the barrier that
-// precedes tile t + 2's DMA), V in the 4-slot ring, and per wave and block one
-// 4-KiB M block staged in LDS by LDS-DMA: 112 + 32 + 4 KiB.
-constexpr int W64_KSLOT_TRI = 3;
-constexpr size_t W64_RING_TRI = (size_t)W64_KSLOT_TRI * H3_KTB + (size_t)W64_NSLOT * H3_VTB;  // 112 KiB
-constexpr size_t W64_MLDS_TRI = (size_t)4 * 2 * MPACK_T * MPACK_T * sizeof(float);             // 32 KiB
-constexpr size_t W64_LDS_TRI = W64_RING_TRI + W64_MLDS_TRI + W64_MAXT * sizeof(float);
-template <bool TRI> constexpr size_t w64_lds_bytes() { return TRI ? W64_LDS_TRI : W64_LDS; }
-// M values of register r: the fragment path's 4 quads or the TRI path's 16 floats
-PDSC_DEV float w64_mget(const f32x4 (&m)[4], int r) { return m[r >> 2][r & 3]; }
-PDSC_DEV float w64_mget(const float (&m)[16], int r) { return m[r]; }
 
 // ---- the accumulator file, asm-owned ----------------------------------------
 // The wave's Q fragments and O accumulators (256 registers) live in fixed
@@ -207,7 +195,6 @@ inline AttnGridH3 attention_w64_grid(int B, int N, int slots) { return attention
 // (sched_barrier-fenced: hipcc neither knows the asm MFMA's 32 cycles nor may
 // it move the slices), the K / V fragments read two k-steps ahead, across
 // region boundaries.  The K/V ring has 4 slots (V(t-1) is read in tile t).
-template <bool TRI>
 PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks,
                                  const _Float16 *__restrict__ Vs, const float *__restrict__ vexp,
                                  const float *__restrict__ M, const AttnGridH3 &g, const AttnBlock &blk, char *smem,
@@ -222,7 +209,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
     const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
     const int mnt = mpack_ntile(g.N);  // M's layout is the batch stride's
-    const size_t mper = TRI ? mpack_floats(g.N) : mfrag_floats(g.N);
+    const size_t mper = mfrag_floats(g.N);
 #ifdef W64_EXP_MSHARED  // diagnostic: every pair reads pair 0's M (L2 / MALL resident)
     const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M, (uint32_t)(mper * 4u));
 #else
@@ -258,19 +245,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         });
     });
 
-    // the ring: K and V of tile st (TRI: K in 3 slots, V in 4; else 4 slots of K + V)
-    auto kslot = [&](int st) -> char * {
-        if constexpr (TRI)
-            return smem + ((st - st0) % W64_KSLOT_TRI) * H3_KTB;
-        else
-            return smem + ((st - st0) & (W64_NSLOT - 1)) * (H3_KTB + H3_VTB);
-    };
-    auto vslot = [&](int st) -> char * {
-        if constexpr (TRI)
-            return smem + W64_KSLOT_TRI * H3_KTB + ((st - st0) & (W64_NSLOT - 1)) * H3_VTB;
-        else
-            return kslot(st) + H3_KTB;
-    };
+    auto slot_of = [&](int st) { return smem + ((st - st0) & (W64_NSLOT - 1)) * (H3_KTB + H3_VTB); };
     // LDS-DMA piece i (0 .. 7) of this wave's share of tile st.  Issued
     // unconditionally (a tile past the split's end reads past the K/V resource,
     // or a tile nobody reads: zeros or unused bytes into a free slot) -- a branch
@@ -281,9 +256,8 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     static_assert(H3_KTB == H3_VTB && W64_NW * DMA_PW == 2 * H3_KTB / 1024, "K / V split over the waves");
     const __amdgpu_buffer_rsrc_t rS = wave < W64_NW / 2 ? rK : rV;
     const int pbase = (wave * DMA_PW) % (H3_KTB / 1024);  // this wave's first piece within its K or V tile
-    const bool kwave = wave < W64_NW / 2;
     auto stage_piece = [&](int st, int i) {
-        char *dst = (kwave ? kslot(st) : vslot(st)) + (pbase + i) * 1024;
+        char *dst = slot_of(st) + (wave * DMA_PW + i) * 1024;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void *)dst, 16, 16 * lane,
                                                  st * H3_KTB + (pbase + i) * 1024, 0, 0);
     };
@@ -292,40 +266,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     auto load_mq = [&](int st, int u, int gg) {  // (qt past the layout: zeros)
         return w64_mload(rM, (uint32_t)(mfrag_off((q0 >> 5) + u, st, mnt) * 4) + 64u * lane + 16u * gg);
     };
-    // TRI: this wave's two M blocks in LDS (block u at mreg + 4 KiB u), copied as
-    // 16-B chunks XOR-swizzled within each lane's 64 B (chunk g of lane l at
-    // 4 l + (g ^ ((l >> 2) & 3))): both read shapes below conflict-free or 2-way
-    char *mreg = smem + W64_RING_TRI + (size_t)wave * 2 * (MPACK_T * MPACK_T * 4);
-    const uint32_t mswz = 16u * (4u * (lane >> 2) + ((lane & 3) ^ ((lane >> 4) & 3)));
-    // M of tile st, block u: 4 KiB by LDS-DMA, piece p (1 KiB) of the block
-    // (qt, kt) (kt <= qt) or (kt, qt) -- the same copy either way
-    auto mdma = [&](int st, int u, int p) {
-        const int qt = (q0 >> 5) + u, kt = st;
-        const uint32_t blk = (uint32_t)(kt <= qt ? mtri_block(qt, kt) : mtri_block(kt, qt));
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rM, (__attribute__((address_space(3))) void *)(mreg + u * (MPACK_T * MPACK_T * 4) + p * 1024), 16, mswz,
-            blk * (MPACK_T * MPACK_T * 4) + p * 1024, 0, 0);
-    };
-    // this lane's 16 M values of tile st, block u, from LDS (after its DMA landed)
-    const int l32 = lane & 31, mhp = (l32 >> 2) & 1, mrp = (l32 & 3) + 4 * (l32 >> 3);
-    auto mread = [&](int st, int u, float (&mv)[16]) {
-        const int qt = (q0 >> 5) + u, kt = st;
-        const float *L = reinterpret_cast<const float *>(mreg + u * (MPACK_T * MPACK_T * 4));
-        if (kt <= qt) {  // block (qt, kt): the lane's own 4 chunks (wave-uniform branch)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const f32x4 v = *reinterpret_cast<const f32x4 *>(L + 4 * (4 * lane + (gg ^ ((lane >> 2) & 3))));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) mv[4 * gg + e] = v[e];
-            }
-        } else {  // block (kt, qt) transposed: register r' = mrp of lanes 32 mhp + acc_row(r, h)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                mv[r] = L[16 * (32 * mhp + 4 * h) + 16 * ((r & 3) + 8 * (r >> 2)) +
-                          4 * ((mrp >> 2) ^ ((2 * (r >> 2) + h) & 3)) + (mrp & 3)];
-        }
-    };
-    const float *ev_lds = reinterpret_cast<const float *>(smem + (TRI ? W64_RING_TRI + W64_MLDS_TRI : W64_RING));
+    const float *ev_lds = reinterpret_cast<const float *>(smem + W64_RING);
     auto load_ev = [&](int st) { return ev_lds[st]; };  // (wave-uniform address: one broadcast read)
 
 #ifdef W64_EXP_NO_LDSREAD  // diagnostic: fragments read once, then reused (no ds_read in the loop)
@@ -355,7 +296,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     // softmax part 1, slice k (0 .. 23) of block u (tile key0, its M and ev):
     // p = M S - base (one fma), the tile's max, the re-base test (attention_h3_core
     // arithmetic, not the first tile)
-    auto sm1_slice = [&](auto kc, int u, const f32x16 &S, const auto &mv, float ev, int key0, SmA &a) {
+    auto sm1_slice = [&](auto kc, int u, const f32x16 &S, const f32x4 (&mv)[4], float ev, int key0, SmA &a) {
         constexpr int k = decltype(kc)::value;
 #ifdef W64_EXP_NO_SM1  // diagnostic: no part-1 VALU (p = S)
         if constexpr (k >= 1 && k <= 16) a.p[k - 1] = S[k - 1];
@@ -368,7 +309,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
             w64_pin(a.mb0);
         } else if constexpr (k <= 16) {
             constexpr int r = k - 1;
-            a.p[r] = __builtin_fmaf(w64_mget(mv, r), S[r], -a.mb0);
+            a.p[r] = __builtin_fmaf(mv[r >> 2][r & 3], S[r], -a.mb0);
             w64_pin(a.p[r]);
         } else if constexpr (k <= 20) {
             if constexpr (k == 17) {
@@ -404,13 +345,13 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         }
     };
     // the first tile's part 1 (m_run = -inf, O = 0: attention_h3_core's first-tile arithmetic)
-    auto sm1_first = [&](int u, const f32x16 &S, const auto &mv, float ev, int key0, SmA &a) {
+    auto sm1_first = [&](int u, const f32x16 &S, const f32x4 (&mv)[4], float ev, int key0, SmA &a) {
         const float scale = ATT_QFMA ? 1.0f : H3_QSCALE;
         float mx = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r) a.p[r] = S[r] * scale;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a.p[r] = w64_mget(mv, r) * a.p[r];
+        for (int r = 0; r < 16; ++r) a.p[r] = mv[r >> 2][r & 3] * a.p[r];
         if (key0 + 32 > N) {
 #pragma unroll
             for (int r = 0; r < 16; ++r)
@@ -555,8 +496,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         __builtin_amdgcn_s_barrier();
     };
 
-    f32x4 mX[2][4], mY[2][4];  // (the fragment path: M of this tile / the next, in registers)
-    float mvA[16], mvB[16];    // (TRI: this tile's M of block A / B, read from LDS)
+    f32x4 mX[2][4], mY[2][4];
     float eX, eY;
     f32x16 S[2];
     SmA sa[2];
@@ -568,30 +508,14 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     // pieces 4-7 (slices 1, 4, 7, 10: M; 13, 16, 19, 22: DMA).  Static counts:
     // a block's M wait finds 12 younger ops (its half's 4 pieces, the other
     // half's 8), the barrier 8 (R2's).
-    // TRI: the 4 DMA pieces first (slices 1, 4, 7, 10), then the block's M
-    // pieces of tile tn (13, 16, 19, 22) into its LDS block, whose reads for this
-    // tile were issued in the previous region (lgkmcnt(4) before the first: every
-    // LDS op but the region's last two fragment reads done -- the M reads among them)
     auto issue_half = [&](auto kc, auto hc, int tn, int td, f32x4 (&mn)[2][4]) {
         constexpr int k = decltype(kc)::value, half = decltype(hc)::value;
-        if constexpr (TRI) {
-            if constexpr (k % 3 == 1 && k <= 10) stage_piece(td, 4 * half + k / 3);
-            if constexpr (k == 13) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-            if constexpr (k % 3 == 1 && k >= 13) mdma(tn, half, (k - 13) / 3);
-        } else {
 #ifndef W64_EXP_NO_M
-            if constexpr (k % 3 == 1 && k <= 10) mn[half][k / 3] = load_mq(tn, half, k / 3);
+        if constexpr (k % 3 == 1 && k <= 10) mn[half][k / 3] = load_mq(tn, half, k / 3);
 #endif
 #ifndef W64_EXP_NO_DMA
-            if constexpr (k % 3 == 1 && k >= 13) stage_piece(td, 4 * half + (k - 13) / 3);
+        if constexpr (k % 3 == 1 && k >= 13) stage_piece(td, 4 * half + (k - 13) / 3);
 #endif
-        }
-    };
-    // TRI: block u's M DMA of this tile landed (8 younger vector-memory ops: the
-    // other block's 4 pieces and its region's 4 DMA pieces), then its LDS reads
-    auto m_ready = [&](int st, int u, float (&mv)[16]) {
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        mread(st, u, mv);
     };
     using H0 = std::integral_constant<int, 0>;
     using H1 = std::integral_constant<int, 1>;
@@ -601,34 +525,23 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     for (int i = 0; i < DMA_PW; ++i) stage_piece(st0, i);
 #pragma unroll
     for (int i = 0; i < DMA_PW; ++i) stage_piece(st0 + 1, i);
-    if constexpr (TRI) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int p = 0; p < 4; ++p) mdma(st0, u, p);
-    } else {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) mX[u][gg] = load_mq(st0, u, gg);
-    }
+        for (int gg = 0; gg < 4; ++gg) mX[u][gg] = load_mq(st0, u, gg);
     {
-        float *evw = const_cast<float *>(ev_lds);
+        float *evw = reinterpret_cast<float *>(smem + W64_RING);
         for (int i = threadIdx.x; i < Npad / H3_TILE; i += W64_NW * 64) evw[i] = vexp_b[i];
     }
-    if constexpr (!TRI) w64_mwait<0>(mX);  // (the Q and M loads are asm: hipcc does not count them)
-    __builtin_amdgcn_s_waitcnt(0x0070);    // vmcnt(0) lgkmcnt(0)
+    w64_mwait<0>(mX);  // (the Q and M loads are asm: hipcc does not count them)
+    __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0) lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     eX = load_ev(st0);
-    if constexpr (TRI) {
-        mread(st0, 0, mvA);
-        mread(st0, 1, mvB);
-    }
 
     // ---- tile st0 (the first: m_run = -inf, O = 0) ----
     {
         const int t = st0, key0 = t * H3_TILE;
-        const char *L = kslot(t), *LV = vslot(t);
+        const char *L = slot_of(t);
         kread(L, 0, kf.f[0]);
         kread(L, 1, kf.f[1]);
         // R1: QK_A
@@ -638,21 +551,15 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         eY = load_ev(min(t + 1, st1 - 1));
         kread(L, 0, kf.f[0]);  // (QK_A's last k-steps held kf[0], kf[1]: R3's first two only now)
         kread(L, 1, kf.f[1]);
-        if constexpr (TRI)
-            sm1_first(0, S[0], mvA, eX, key0, sa[0]);
-        else
-            sm1_first(0, S[0], mX[0], eX, key0, sa[0]);
+        sm1_first(0, S[0], mX[0], eX, key0, sa[0]);
         // R3: QK_B + softmax_A part 2
-        qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(LV),
+        qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(L + H3_KTB),
                   [&](auto kc) { sm2_slice(kc, 0, sa[0], eX, sb, ph[0], pl[0]); });
         mid_barrier();
         // R4: PV_A + softmax_B part 1 (first tile)
-        pv_region(std::integral_constant<int, 0>{}, LV, ph[0], pl[0], next_k(kslot(t + 1)),
+        pv_region(std::integral_constant<int, 0>{}, L + H3_KTB, ph[0], pl[0], next_k(slot_of(t + 1)),
                   [&](auto kc) { issue_half(kc, H1{}, min(t + 1, st1 - 1), t + 2, mY); });
-        if constexpr (TRI)
-            sm1_first(1, S[1], mvB, eX, key0, sa[1]);
-        else
-            sm1_first(1, S[1], mX[1], eX, key0, sa[1]);
+        sm1_first(1, S[1], mX[1], eX, key0, sa[1]);
     }
     // ---- steady state: tile t (its M in mc, ev ec; the next tile's into mn, en) ----
     auto tile = [&](int t, f32x4 (&mc)[2][4], float &ec, float &ep, f32x4 (&mn)[2][4], float &en) {
@@ -660,43 +567,32 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         const int si = W64_ST_PER_TILE * min(t - st0, 39);
         (void)si;
         W64_ST(si);
-        const char *L = kslot(t), *LV = vslot(t), *LVp = vslot(t - 1);
+        const char *L = slot_of(t), *Lp = slot_of(t - 1);
         // R1: QK_A(t) + softmax_B(t - 1) part 2 (ep: tile t - 1's V exponent)
-        // (TRI: + block A's M of tile t out of LDS, 8 slices ahead of its use)
-        qk_region(std::integral_constant<int, 0>{}, L, S[0], next_v(LVp), [&](auto kc) {
-            sm2_slice(kc, 1, sa[1], ep, sb, ph[1], pl[1]);
-            if constexpr (TRI && decltype(kc)::value == 15) m_ready(t, 0, mvA);
-        });
+        qk_region(std::integral_constant<int, 0>{}, L, S[0], next_v(Lp + H3_KTB),
+                  [&](auto kc) { sm2_slice(kc, 1, sa[1], ep, sb, ph[1], pl[1]); });
         W64_ST(si + 1);
         // R2: PV_B(t - 1) + softmax_A(t) part 1 + tile t + 1's M, tile t + 2's DMA
-        pv_region(std::integral_constant<int, 1>{}, LVp, ph[1], pl[1], next_k(L), [&](auto kc) {
+        pv_region(std::integral_constant<int, 1>{}, Lp + H3_KTB, ph[1], pl[1], next_k(L), [&](auto kc) {
             // block A's M of tile t (issued in R2 of tile t - 1; 12 younger ops)
-            if constexpr (!TRI && decltype(kc)::value == 0) w64_mwait_blk<12>(mc[0]);
+            if constexpr (decltype(kc)::value == 0) w64_mwait_blk<12>(mc[0]);
             if constexpr (decltype(kc)::value == 2) en = load_ev(min(t + 1, st1 - 1));
-            if constexpr (TRI)
-                sm1_slice(kc, 0, S[0], mvA, ec, key0, sa[0]);
-            else
-                sm1_slice(kc, 0, S[0], mc[0], ec, key0, sa[0]);
+            sm1_slice(kc, 0, S[0], mc[0], ec, key0, sa[0]);
             issue_half(kc, H0{}, min(t + 1, st1 - 1), t + 2, mn);
         });
         rebase(std::integral_constant<int, 0>{}, sa[0]);
         W64_ST(si + 2);
-        // R3: QK_B(t) + softmax_A(t) part 2 (TRI: + block B's M of tile t)
-        qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(LV), [&](auto kc) {
-            sm2_slice(kc, 0, sa[0], ec, sb, ph[0], pl[0]);
-            if constexpr (TRI && decltype(kc)::value == 15) m_ready(t, 1, mvB);
-        });
+        // R3: QK_B(t) + softmax_A(t) part 2
+        qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(L + H3_KTB),
+                  [&](auto kc) { sm2_slice(kc, 0, sa[0], ec, sb, ph[0], pl[0]); });
         W64_ST(si + 3);
         mid_barrier();
         W64_ST(si + 4);
         // R4: PV_A(t) + softmax_B(t) part 1
-        pv_region(std::integral_constant<int, 0>{}, LV, ph[0], pl[0], next_k(kslot(t + 1)), [&](auto kc) {
+        pv_region(std::integral_constant<int, 0>{}, L + H3_KTB, ph[0], pl[0], next_k(slot_of(t + 1)), [&](auto kc) {
             // block B's M of tile t (issued in R4 of tile t - 1; 12 younger ops)
-            if constexpr (!TRI && decltype(kc)::value == 0) w64_mwait_blk<12>(mc[1]);
-            if constexpr (TRI)
-                sm1_slice(kc, 1, S[1], mvB, ec, key0, sa[1]);
-            else
-                sm1_slice(kc, 1, S[1], mc[1], ec, key0, sa[1]);
+            if constexpr (decltype(kc)::value == 0) w64_mwait_blk<12>(mc[1]);
+            sm1_slice(kc, 1, S[1], mc[1], ec, key0, sa[1]);
             issue_half(kc, H1{}, min(t + 1, st1 - 1), t + 2, mn);
         });
         rebase(std::integral_constant<int, 1>{}, sa[1]);
@@ -720,17 +616,15 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     // The last tile loaded a "next" M that nothing reads: its registers must stay
     // allocated until the asm loads have landed (hipcc would otherwise hand them
     // to the V fragments below, and the late loads would overwrite those).
-    if constexpr (!TRI) {
-        w64_mwait<0>(mX);
-        w64_mwait<0>(mY);
-    }
+    w64_mwait<0>(mX);
+    w64_mwait<0>(mY);
     {
         const float el = ((t - st0) & 1) ? eX : eY;  // the last tile's exponent
-        const char *LVp = vslot(t - 1);
+        const char *Lp = slot_of(t - 1);
         static_for<24>([&](auto kc) { sm2_slice(kc, 1, sa[1], el, sb, ph[1], pl[1]); });
-        vread(LVp, 0, vf.f[0]);
-        vread(LVp, 1, vf.f[1]);
-        pv_region(std::integral_constant<int, 1>{}, LVp, ph[1], pl[1], none, none);
+        vread(Lp + H3_KTB, 0, vf.f[0]);
+        vread(Lp + H3_KTB, 1, vf.f[1]);
+        pv_region(std::integral_constant<int, 1>{}, Lp + H3_KTB, ph[1], pl[1], none, none);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) l_run[u] = halves_sum(l_run[u]);
@@ -793,8 +687,7 @@ PDSC_DEV void w64_store_partial(const AttnGridH3 &g, const AttnBlock &blk, float
 }
 
 // Split-K attention with 64-query waves: partials as attention_h3_kernel.
-// TRI: M in the triangular fragment order (else the dense fragment order).
-template <bool XCD, bool TRI>
+template <bool XCD>
 __global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
@@ -804,7 +697,7 @@ __global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
     if (blk.qb * W64_QPB >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
     const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     float m_run[2], l_run[2];
-    attention_w64_core<TRI>(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
+    attention_w64_core(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
     w64_store_partial(g, blk, opart, ml, wave, lane, m_run, l_run);
 }
 
@@ -842,7 +735,7 @@ PDSC_DEV void w64_zero_partial(const AttnGridH3 &g, int b, int qb, int s, float 
     }
 }
 
-template <bool XCD, bool TRI>
+template <bool XCD>
 __global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_sk_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, int nwg, float *__restrict__ opart,
@@ -862,7 +755,7 @@ __global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_sk_kernel(
         blk.st1 = (int)(x1 - k0);
         __builtin_amdgcn_s_waitcnt(0x0070);  // the previous segment's stores: the core starts with none in flight
         float m_run[2], l_run[2];
-        attention_w64_core<TRI>(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
+        attention_w64_core(Qs, Ks, Vs, vexp, M, g, blk, w64smem, wave, lane, m_run, l_run);
         w64_store_partial(g, blk, opart, ml, wave, lane, m_run, l_run);
         if (x1 == k0 + nst)
             for (int s = blk.split + 1; s < g.nsplit; ++s) w64_zero_partial(g, blk.b, blk.qb, s, opart, ml, tid);

@@ -180,25 +180,21 @@ __global__ __launch_bounds__(256) void compat_kernel(const float *__restrict__ s
     }
 }
 
-// The forward's M, symmetric-packed: PDSC_MTRI (default) the triangular
-// fragment order (pdsc_internal.hpp, mtri_block) -- each 32 x 32 block with
-// kt <= qt as the attention's S^T accumulator lane order, one contiguous 4 KiB
-// block; PDSC_MTRI = 0 the r01-r04 row-major tiles (mpack_tile).  Half the
-// bytes of the dense matrix either way.  A workgroup computes a 64 x 64
-// upper-triangle block (ti <= tj) like the dense kernel (compat4), stages it in
-// LDS and stores its 32 x 32 tiles (three on the diagonal) as 1-KiB wave
-// stores.  (The dense, twice-written form costs 2x the bytes in 256-B segments
-// strided by 4N B: ~2.9 TB/s at N = 5000 against ~5.3 TB/s for contiguous
-// stores, tools/compat_bench.hip.)  Entries past N are written as 0.
+// The forward's M: symmetric-packed 32 x 32 tiles (pdsc_internal.hpp,
+// mpack_tile), each one contiguous 4 KiB block -- half the bytes of the dense
+// matrix, and each block exactly the 32 keys x 32 queries an attention wave
+// reads per step (in either orientation).  A workgroup computes a 64 x 64
+// upper-triangle block (ti <= tj) like the dense kernel and stores its four
+// 32 x 32 tiles (three on the diagonal: the lower one is the transpose of the
+// upper).  (The dense, twice-written form above costs 2x the bytes in 256-B
+// segments strided by 4N B: ~2.9 TB/s at N = 5000 against ~5.3 TB/s for
+// contiguous stores, tools/compat_bench.hip.)  Entries past N are written as 0.
 __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restrict__ src,
                                                             const float *__restrict__ tgt, int Nstr, int ntile,
                                                             const float *__restrict__ sigma_d_ptr,
                                                             float *__restrict__ Mp, Ragged rg) {
     __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
     __shared__ CompatScratch scr[4];
-#if PDSC_MTRI
-    __shared__ float T[CT][CT + 1];  // the 64 x 64 block, rows i, columns j
-#endif
     int t = blockIdx.x, ti = 0;
     while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
     const int tj = ti + t;
@@ -258,34 +254,10 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             if (i0 + r >= N || j0 + cq * 4 + q >= N) out[q] = 0.0f;
-#if PDSC_MTRI
-#pragma unroll
-        for (int q = 0; q < 4; ++q) T[r][cq * 4 + q] = out[q];
-#else
         if (skip) continue;
         float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
         *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{out[0], out[1], out[2], out[3]};
-#endif
     }
-#if PDSC_MTRI
-    __syncthreads();
-    // wave w: the 32 x 32 tile (sr, sc) = (w >> 1, w & 1) of the block, stored
-    // when tr <= tc as the fragment block (qt = tc, kt = tr) (keys = rows i);
-    // store g: lane L writes block-lane 16 g + L / 4's registers 4 (L % 4) .. + 3
-    // = 4 consecutive keys e + 8 c + 4 h of its query (1 KiB per wave store)
-    const int sr = wave >> 1, sc = wave & 1;
-    const int tr = 2 * ti + sr, tcc = 2 * tj + sc;
-    if (tr > tcc || tr >= nt32 || tcc >= nt32) return;  // wave-uniform
-    float *blk = Mb + mtri_block(tcc, tr) * (MPACK_T * MPACK_T);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int bl = 16 * g + (lane >> 2), c = lane & 3, hh = bl >> 5, q = bl & 31;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = T[32 * sr + e + 8 * c + 4 * hh][32 * sc + q];
-        *reinterpret_cast<f32x4 *>(blk + 256 * g + 4 * lane) = f32x4{v[0], v[1], v[2], v[3]};
-    }
-#endif
 }
 
 // The h3 forward's M in the fragment order of attention_w64 (pdsc_internal.hpp,

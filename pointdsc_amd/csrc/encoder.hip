@@ -183,14 +183,6 @@ static int w64_nsplit(int B, int N) {
     return nwg ? std::max(g.nsplit, w64_sk_nsplit(B, g.nqb, (N + H3_TILE - 1) / H3_TILE, nwg)) : g.nsplit;
 }
 
-bool w64_mtri() {
-    static const bool on = [] {
-        const char *e = getenv("PDSC_W64_MTRI");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 int attention_nsplit(int B, int N, bool f32, bool w64) {
     return f32 ? f32_grid(B, N).nsplit : (w64 ? w64_nsplit(B, N) : prod_grid(B, N).nsplit);
 }
@@ -199,33 +191,23 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
                             int m_layout, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
                             hipStream_t s, Ragged rg) {
     const bool m_packed = m_layout == M_PACKED;
-    if (m_layout == M_FRAG || m_layout == M_TRI_W64) {  // attention_w64 (H3 layouts; dense-fragment or triangular M)
+    if (m_layout == M_FRAG) {  // attention_w64 (H3 layouts, fragment-ordered M)
         if (f32) return hipErrorInvalidValue;
         AttnGridH3 g = w64_grid(B, N);
         if (g.Npad != Npad || nsplit != w64_nsplit(B, N)) return hipErrorInvalidValue;
         g.nsplit = nsplit;  // slots past the split grid's own: empty splits (st0 >= st1)
         const int nwg = rg.nv ? 0 : w64_sk_wgs(B, N);
-        const _Float16 *qs = static_cast<const _Float16 *>(q), *ks = static_cast<const _Float16 *>(k),
-                       *vs = static_cast<const _Float16 *>(v);
-        const bool tri = m_layout == M_TRI_W64;
         if (nwg) {
-            if (tri)
-                hipLaunchKernelGGL((attention_w64_sk_kernel<true, true>), dim3(nwg), dim3(W64_NW * 64),
-                                   w64_lds_bytes<true>(), s, qs, ks, vs, vexp, M, g, nwg, opart, ml);
-            else
-                hipLaunchKernelGGL((attention_w64_sk_kernel<true, false>), dim3(nwg), dim3(W64_NW * 64),
-                                   w64_lds_bytes<false>(), s, qs, ks, vs, vexp, M, g, nwg, opart, ml);
+            hipLaunchKernelGGL((attention_w64_sk_kernel<true>), dim3(nwg), dim3(W64_NW * 64), W64_LDS, s,
+                               static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
+                               static_cast<const _Float16 *>(v), vexp, M, g, nwg, opart, ml);
             return hipGetLastError();
         }
         g.nv = rg.nv;
         g.po = rg.po;
-        const dim3 grid(g.B * g.nqb * g.nsplit);
-        if (tri)
-            hipLaunchKernelGGL((attention_w64_kernel<true, true>), grid, dim3(W64_NW * 64), w64_lds_bytes<true>(), s, qs,
-                               ks, vs, vexp, M, g, opart, ml);
-        else
-            hipLaunchKernelGGL((attention_w64_kernel<true, false>), grid, dim3(W64_NW * 64), w64_lds_bytes<false>(), s,
-                               qs, ks, vs, vexp, M, g, opart, ml);
+        hipLaunchKernelGGL((attention_w64_kernel<true>), dim3(g.B * g.nqb * g.nsplit), dim3(W64_NW * 64), W64_LDS, s,
+                           static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
+                           static_cast<const _Float16 *>(v), vexp, M, g, opart, ml);
         return hipGetLastError();
     }
     if (f32) {  // fp32 [B][Npad][CH] rows, dense M

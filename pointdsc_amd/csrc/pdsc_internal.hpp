@@ -39,20 +39,6 @@ __host__ __device__ inline size_t mfrag_floats(int N) {
     return nt * nt * MPACK_T * MPACK_T;
 }
 __host__ __device__ inline size_t mfrag_off(int qt, int kt, int nt) { return ((size_t)qt * nt + kt) * (MPACK_T * MPACK_T); }
-// ---- triangular fragment-ordered M (the h3 forward's a1 output, PDSC_MTRI) ---
-// The symmetric M stored once: for each pair of 32-tiles a >= b only the block
-// (query tile qt = a, key tile kt = b) of the fragment order above (64 lanes x 16
-// floats, lane (h, q) holding M[32 b + acc_row(r, h)][32 a + q]), blocks in
-// lower-triangle row-major order: index a (a + 1) / 2 + b.  mpack_floats(N)
-// floats per pair -- half the dense bytes.  A wave reads block (qt, kt), kt <= qt,
-// as 4 contiguous 16-B loads per lane (1 KiB per wave instruction); block
-// (qt, kt), kt > qt, is block (kt, qt) transposed: lane (h, q) reads register
-// r' = (q & 3) + 4 (q >> 3) of lanes 32 ((q >> 2) & 1) + acc_row(r, h), r = 0..15
-// -- 16 dword loads, each wave instruction four whole 64-B segments.
-#ifndef PDSC_MTRI
-#define PDSC_MTRI 1  // 0: the r01-r04 row-major packed tiles (mpack_tile), A/B builds only
-#endif
-__host__ __device__ inline size_t mtri_block(int a, int b) { return (size_t)a * (a + 1) / 2 + b; }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 
 // fp16 planes per packed 1x1-conv weight (3xfp16 mode): 2 = hi + mid (22
@@ -181,8 +167,7 @@ hipError_t launch_ragged_order(const int32_t *counts_host, int B, int *po, hipSt
 // ---- launchers --------------------------------------------------------------
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,
                          float *M, hipStream_t s, Ragged rg = {});
-// Mp: [B][mpack_floats(N)]: the triangular fragment order (mtri_block; PDSC_MTRI = 0:
-// the row-major packed tiles, mpack_tile)
+// Mp: [B][mpack_floats(N)]
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
                                 float *Mp, hipStream_t s, Ragged rg = {});
 
@@ -201,13 +186,8 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 // the split path's attention as attention_w64 (fragment-ordered M) for this shape?
 bool attention_w64(int B, int N, bool f32);
 int attention_nsplit(int B, int N, bool f32, bool w64 = false);
-// M's layouts: dense [B][N][N], symmetric-packed (mpack_floats: the triangular
-// fragment order, mtri_block), fragment-ordered (mfrag_*); M_TRI_W64 is M_PACKED's
-// bytes for the attention_w64 plan
-enum MLayout { M_DENSE = 0, M_PACKED = 1, M_FRAG = 2, M_TRI_W64 = 3 };
-// the w64 plan's M: the triangular order (default) or the dense fragment order
-// (knob PDSC_W64_MTRI=0, measurement only)
-bool w64_mtri();
+// M's layouts: dense [B][N][N], symmetric-packed (mpack_*), fragment-ordered (mfrag_*)
+enum MLayout { M_DENSE = 0, M_PACKED = 1, M_FRAG = 2 };
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
 // or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
 // M: dense [B][N][N], symmetric-packed [B][mpack_floats(N)] (H3) or fragment-ordered

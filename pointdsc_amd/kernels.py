@@ -81,22 +81,13 @@ def compat_packed(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -
     Mp = torch.empty((B, nf), dtype=torch.float32, device=src.device)
     check(L.pdsc_compat_packed_f32(_p(src), _p(tgt), B, N, _p(sigma_d), _p(Mp), _stream(src.device)),
           "pdsc_compat_packed_f32")
-    return unpack_tri(Mp, N)
-
-
-def unpack_tri(Mp: torch.Tensor, N: int) -> torch.Tensor:
-    """[B, mpack_floats(N)] in the triangular fragment order (pdsc_internal.hpp,
-    mtri_block) -> dense [B,N,N]: block (a, b), a >= b, at a(a+1)/2 + b holds
-    M[32b + acc_row(r, h)][32a + q] at lane (h, q) = 32h + q, register r."""
     T = 32
-    B = Mp.shape[0]
     nt = (N + T - 1) // T
-    a, b = torch.tril_indices(nt, nt, device=Mp.device)  # a >= b, row-major: index a(a+1)/2 + b
-    F = Mp.view(B, -1, 2, 32, 4, 4)  # block, h, q, r // 4 (g), r % 4 (e): row 32b + e + 8g + 4h, column 32a + q
-    blocks = F.permute(0, 1, 4, 2, 5, 3).reshape(B, -1, T, T)  # block, (g, h, e) = row in tile, q = column
-    full = torch.zeros((B, nt, nt, T, T), dtype=torch.float32, device=Mp.device)
-    full[:, b, a] = blocks  # rows = key tile b, columns = query tile a
-    full[:, a, b] = blocks.transpose(-1, -2)
+    ti, tj = torch.triu_indices(nt, nt)
+    tiles = Mp.view(B, -1, T, T)  # upper-triangle tiles in row-major (ti, tj) order
+    full = torch.zeros((B, nt, nt, T, T), dtype=torch.float32, device=src.device)
+    full[:, ti, tj] = tiles
+    full[:, tj, ti] = tiles.transpose(-1, -2)
     return full.permute(0, 1, 3, 2, 4).reshape(B, nt * T, nt * T)[:, :N, :N].contiguous()
 
 

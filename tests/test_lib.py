@@ -159,29 +159,3 @@ def test_flat_weight_views_track_edits():
     e = mod._REGISTRATION_EPOCH[0]
     m.classification[4].bias = nn.Parameter(torch.zeros(1))
     assert mod._REGISTRATION_EPOCH[0] != e
-
-
-def test_unpack_tri_layout():
-    """kernels.unpack_tri inverts the triangular fragment order of the forward's M
-    (pdsc_internal.hpp, mtri_block): block (a, b), a >= b, lane (h, q), register r
-    holds M[32 b + acc_row(r, h)][32 a + q], acc_row(r, h) = r%4 + 8 (r/4) + 4 h."""
-    import torch
-    from pointdsc_amd.kernels import unpack_tri
-    rng = np.random.default_rng(3)
-    for N in (40, 77, 96):
-        nt = (N + 31) // 32
-        M = rng.random((nt * 32, nt * 32)).astype(np.float32)
-        M = M + M.T
-        M[N:] = 0
-        M[:, N:] = 0
-        Mp = np.zeros(nt * (nt + 1) // 2 * 1024, np.float32)
-        for a in range(nt):
-            for b in range(a + 1):
-                base = (a * (a + 1) // 2 + b) * 1024
-                for lane in range(64):
-                    h, q = lane // 32, lane % 32
-                    for r in range(16):
-                        row = r % 4 + 8 * (r // 4) + 4 * h
-                        Mp[base + lane * 16 + r] = M[32 * b + row, 32 * a + q]
-        out = unpack_tri(torch.from_numpy(Mp)[None], N)[0].numpy()
-        assert np.array_equal(out, M[:N, :N]), N

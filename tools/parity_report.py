@@ -75,6 +75,13 @@ def report(name, precision, dev):
     out["seed_min_gap_ref"] = float(g["seed_score_min_gap"])
     out["trans_abs"] = float(np.abs(trans[0].cpu().numpy() - g["final_trans"]).max())
     out["label_mismatch"] = int((labels[0].cpu().numpy() != g["final_labels"]).sum())
+    if precision == "h3":  # the same inputs through the exact-fp32 contractions
+        cfg32, packed32 = m.pdsc_config("f32"), m.packed_weights("f32")
+        T32, L32, c32, _ = kernels.forward_testing(cfg32, packed32, corr, src, tgt, debug=True)
+        out["h3_vs_f32_logit"] = float((conf2[0].double() - c32[0].double()).abs().max())
+        out["h3_vs_f32_pose"] = float((trans[0] - T32[0]).abs().max())
+        out["h3_vs_f32_labels"] = int((labels[0] != L32[0]).sum())
+        out["f32_trans_abs"] = float(np.abs(T32[0].cpu().numpy() - g["final_trans"]).max())
     if not has_f:
         return out
     # stage-isolated NSM chain on the reference's own normed / seeds
