@@ -33,7 +33,7 @@ def report(name, precision, dev):
     from pointdsc_amd.PointDSC import PointDSC
     g = load_golden(name)
     hp = golden_hparams(g)
-    m = PointDSC(in_dim=6, num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
+    m = PointDSC(in_dim=hp["in_dim"], num_layers=hp["num_layers"], num_channels=128, num_iterations=10, ratio=0.1,
                  inlier_threshold=hp["inlier_threshold"], sigma_d=float(g["sigma_d"]), k=40,
                  nms_radius=hp["nms_radius"], precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in golden_state_dict(g).items()})
