@@ -211,7 +211,7 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
 // S and M ready, softmax done, PV issued, barrier passed; then the chain phase.
 // Stamps go to a buffer of their own that nothing in the kernel reads.
 #ifdef ATT_STAMPS
-constexpr int ST_PER_WAVE = 192, ST_WGS = 64;
+constexpr int ST_PER_WAVE = 256, ST_WGS = 64;  // (192 + 3 c .. : the fused chain's chunk c, w2_layer)
 static __device__ unsigned long long g_att_stamps[ST_WGS * 4 * ST_PER_WAVE];
 PDSC_DEV unsigned long long *att_stamp_ptr(int wave) {
     return (blockIdx.x % 16 == 0 && blockIdx.x / 16 < ST_WGS && wave < 4)

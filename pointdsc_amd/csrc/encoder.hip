@@ -1166,11 +1166,14 @@ PDSC_DEV void w2_layer(W2Pipe &P, const float *pk, const W2Sched &S, const f16x8
     static_assert(NCH * NT == OUT / 32, "chunk tiling");
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
+        CH_STAMP(192 + 3 * min(P.c, 20));  // (diagnostic build: chunk P.c's MFMAs, its sync, tools/att_stamps.py)
         if (active) w2_mma<NKS, NT, TRANS>(P.slot(P.c), xh, xl, acc, c * NT, lane);
+        CH_STAMP(193 + 3 * min(P.c, 20));
         if (c == 0)
             w2_sync<NST>(active);
         else
             w2_sync<0>(active);
+        CH_STAMP(194 + 3 * min(P.c, 20));
         w2_stage(pk, S, P.c + PW2_NSLOT, P.slot(P.c), wave, lane);
         asm volatile("" ::: "memory");
         ++P.c;

@@ -18,7 +18,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-ST_PER_WAVE, ST_WGS = 192, 64
+ST_PER_WAVE, ST_WGS = 256, 64
 
 
 def main():
@@ -71,6 +71,18 @@ def main():
                          "chain_layers_us": {nm: float(us(n[:, :, b] - n[:, :, a]).mean()) for nm, a, b in
                                              [("fc0", 171, 172), ("fc3", 172, 173), ("fc6", 173, 174), ("pcn", 174, 175),
                                               ("q", 175, 176), ("k", 176, 177), ("v", 177, 178), ("tail", 178, 180)]}}
+        # the chain's weight chunks (w2_layer): MFMAs, the sync (DMA wait + barrier), and
+        # the gap to the next chunk (epilogues, stores, the next layer's setup)
+        ch = []
+        for c in range(11):
+            a, b_, e = 192 + 3 * c, 193 + 3 * c, 194 + 3 * c
+            if not (n[:, :, e] > 0).all():
+                break
+            nxt = 192 + 3 * (c + 1) if c < 10 and (n[:, :, 192 + 3 * (c + 1)] > 0).all() else 180
+            ch.append({"chunk": c, "mma_us": round(float(us(n[:, :, b_] - n[:, :, a]).mean()), 3),
+                       "sync_us": round(float(us(n[:, :, e] - n[:, :, b_]).mean()), 3),
+                       "after_us": round(float(us(n[:, :, nxt] - n[:, :, e]).mean()), 3)})
+        rep["normal"]["chain_chunks"] = ch
     if cfirst.any():
         c = st[cfirst]
         rep["chain_first"] = {"chain_us": float(us(c[:, :, 179] - c[:, :, 0]).mean()),

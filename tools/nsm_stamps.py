@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-ST_PER_WAVE, ST_WGS = 192, 64
+ST_PER_WAVE, ST_WGS = 256, 64
 
 
 def main():

@@ -16,7 +16,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-ST_PER_WAVE, ST_WGS = 192, 64
+ST_PER_WAVE, ST_WGS = 256, 64
 
 
 def main():
