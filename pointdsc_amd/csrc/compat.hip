@@ -450,7 +450,9 @@ hipError_t launch_ragged_order(const int32_t *counts, int B, int *po, hipStream_
 constexpr int RAGGED_CHAIN_TILES = 12, RAGGED_SLOTS = 64;
 hipError_t launch_ragged_plan(const int32_t *counts, int B, int nqb, int *wt, hipStream_t s) {
     const int G = B * nqb;
-    if (G % 8 || nqb >= RAGGED_WT_QB - 1) return hipErrorInvalidValue;  // (the fused grid: B x nqb, nqb <= 256)
+    if (nqb >= RAGGED_WT_QB - 1) return hipErrorInvalidValue;  // (the fused grid: B x nqb, nqb <= 256)
+    // attention_h3_block deals logical ids [0, full) to the XCDs in 8 contiguous
+    // ranges of cap; the last G - full (< 8) ids run after them in id order
     struct Job {
         int cost, pair, qb;
     };
@@ -459,8 +461,9 @@ hipError_t launch_ragged_plan(const int32_t *counts, int B, int nqb, int *wt, hi
     std::stable_sort(rank.begin(), rank.end(), [&](int a, int b) { return counts[a] > counts[b]; });
     // pairs -> XCDs: the least loaded XCD with room (its G / 8 logical ids)
     std::vector<std::vector<Job>> xcd(8);
+    std::vector<Job> tail;
     std::vector<long> work(8, 0);
-    const int cap = G / 8;
+    const int full = G & ~7, cap = full / 8;
     for (int p : rank) {
         const int nb = (counts[p] + QB - 1) / QB, cost = (counts[p] + KT - 1) / KT + RAGGED_CHAIN_TILES;
         int best = -1;
@@ -471,6 +474,10 @@ hipError_t launch_ragged_plan(const int32_t *counts, int B, int nqb, int *wt, hi
             if (x < 0)  // no XCD has room for the whole pair: its blocks one by one (sum of nb <= G)
                 for (int y = 0; y < 8; ++y)
                     if ((int)xcd[y].size() < cap && (x < 0 || work[y] < work[x])) x = y;
+            if (x < 0) {  // every range full: the tail ids
+                tail.push_back(Job{cost, p, q});
+                continue;
+            }
             xcd[x].push_back(Job{cost, p, q});
             work[x] += cost;
         }
@@ -515,6 +522,8 @@ hipError_t launch_ragged_plan(const int32_t *counts, int B, int nqb, int *wt, hi
         }
         for (int i = 0; i < J; ++i) table[x * cap + i] = RAGGED_WT(order[i].pair, order[i].qb);
     }
+    if ((int)tail.size() > G - full) return hipErrorInvalidValue;  // (cannot happen: sum of nb <= G)
+    for (size_t i = 0; i < tail.size(); ++i) table[full + i] = RAGGED_WT(tail[i].pair, tail[i].qb);
     for (int i0 = 0; i0 < G; i0 += RAGGED_CHUNK) {
         RaggedChunk c{};
         const int nb = std::min(RAGGED_CHUNK, G - i0);
