@@ -259,15 +259,6 @@ static bool ragged_order_on() {
     }();
     return !off;
 }
-// A/B knob (measurement only): PDSC_RAGGED_PLAN=0 keeps the fused ragged launches
-// in the pair order above (no workgroup table)
-static bool ragged_plan_on() {
-    static const bool off = [] {
-        const char *e = getenv("PDSC_RAGGED_PLAN");
-        return e && e[0] == '0';
-    }();
-    return !off;
-}
 
 struct FwdBufs {
     int *range;  // [B] the fp16 range guard's per-pair flags: the workspace's first bytes (pdsc_range_status)
@@ -275,7 +266,6 @@ struct FwdBufs {
     _Float16 *normed_s;
     int *seeds, *knn, *counts;
     int *nv, *sv, *po;  // ragged batches: per-pair correspondences and seeds, attention pair order
-    int *wt;            // ragged batches on the fused plan: the attention's workgroup table (B * Npad / 128)
     EncBufs enc;
     NsmBufs nsm;
 };
@@ -301,7 +291,6 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     f.nv = c.take<int>((size_t)d.B);
     f.sv = c.take<int>((size_t)d.B);
     f.po = c.take<int>((size_t)d.B);
-    f.wt = c.take<int>((size_t)d.B * (d.Npad / QB));
     return f;
 }
 
@@ -727,10 +716,6 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
         if (ragged_order_on()) {
             HIPCHK(launch_ragged_order(counts, B, f.po, s));
             rg.po = f.po;
-            if (d.fuse && ragged_plan_on()) {  // the fused launches' planned workgroup order
-                HIPCHK(launch_ragged_plan(counts, B, d.Npad / QB, f.wt, s));
-                rg.wt = f.wt;
-            }
         }
     }
     const PackLayout lay = make_layout(cfg->num_layers, cfg->in_dim);

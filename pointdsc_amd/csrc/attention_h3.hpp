@@ -265,7 +265,6 @@ struct AttnGridH3 {
     // ragged batches: pair b's correspondences (N, Npad: the batch's strides), or null
     const int *nv;
     const int *po;  // ragged batches: workgroup pair slot -> pair (Ragged::po), or null
-    const int *wt;  // ragged batches, one key split: logical id -> RAGGED_WT(pair, block) (Ragged::wt), or null
     PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
@@ -299,7 +298,6 @@ inline AttnGridH3 attention_h3_grid(int B, int N, int slots) {
     AttnGridH3 g;
     g.nv = nullptr;
     g.po = nullptr;
-    g.wt = nullptr;
     g.B = B;
     g.N = N;
     g.Npad = round_up(N, QB);
@@ -323,10 +321,6 @@ PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
     if (xcd) {
         const int full = G & ~7;
         if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
-    }
-    if (g.wt) {  // (one split: the launch's planned workgroup order)
-        const int v = g.wt[lid];
-        return AttnBlock{v / RAGGED_WT_QB, v % RAGGED_WT_QB, 0};
     }
     const int slot = lid / g.nsplit / g.nqb;
     return AttnBlock{g.po ? g.po[slot] : slot, (lid / g.nsplit) % g.nqb, lid % g.nsplit};

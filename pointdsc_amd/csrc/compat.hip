@@ -437,101 +437,4 @@ hipError_t launch_ragged_order(const int32_t *counts, int B, int *po, hipStream_
     return hipSuccess;
 }
 
-// The fused ragged attention's workgroup table (pdsc_internal.hpp).  Model: a
-// block of a pair of n correspondences costs ceil(n / 32) key tiles of attention
-// plus ~RAGGED_CHAIN_TILES for its pointwise chain (round-3 stamps: 110 us for
-// 32 tiles + 42 us); an XCD has RAGGED_SLOTS resident workgroups (32 CUs x 2)
-// and starts its blocks in table order, each on the first slot to free up.
-// With at most two blocks per slot, longest-first order pairs each long block
-// with a short one; the few slots that must take a third block (more blocks
-// than two rounds, e.g. 1038 blocks for 128 pairs of N in [700, 1300] against
-// 1024) then get the XCD's three shortest, instead of whatever frees first --
-// a third block behind two long ones (list scheduling: 122 vs 105 tile-units).
-constexpr int RAGGED_CHAIN_TILES = 12, RAGGED_SLOTS = 64;
-hipError_t launch_ragged_plan(const int32_t *counts, int B, int nqb, int *wt, hipStream_t s) {
-    const int G = B * nqb;
-    if (nqb >= RAGGED_WT_QB - 1) return hipErrorInvalidValue;  // (the fused grid: B x nqb, nqb <= 256)
-    // attention_h3_block deals logical ids [0, full) to the XCDs in 8 contiguous
-    // ranges of cap; the last G - full (< 8) ids run after them in id order
-    struct Job {
-        int cost, pair, qb;
-    };
-    std::vector<int> rank(B);
-    for (int b = 0; b < B; ++b) rank[b] = b;
-    std::stable_sort(rank.begin(), rank.end(), [&](int a, int b) { return counts[a] > counts[b]; });
-    // pairs -> XCDs: the least loaded XCD with room (its G / 8 logical ids)
-    std::vector<std::vector<Job>> xcd(8);
-    std::vector<Job> tail;
-    std::vector<long> work(8, 0);
-    const int full = G & ~7, cap = full / 8;
-    for (int p : rank) {
-        const int nb = (counts[p] + QB - 1) / QB, cost = (counts[p] + KT - 1) / KT + RAGGED_CHAIN_TILES;
-        int best = -1;
-        for (int x = 0; x < 8; ++x)
-            if ((int)xcd[x].size() + nb <= cap && (best < 0 || work[x] < work[best])) best = x;
-        for (int q = 0; q < nb; ++q) {
-            int x = best;
-            if (x < 0)  // no XCD has room for the whole pair: its blocks one by one (sum of nb <= G)
-                for (int y = 0; y < 8; ++y)
-                    if ((int)xcd[y].size() < cap && (x < 0 || work[y] < work[x])) x = y;
-            if (x < 0) {  // every range full: the tail ids
-                tail.push_back(Job{cost, p, q});
-                continue;
-            }
-            xcd[x].push_back(Job{cost, p, q});
-            work[x] += cost;
-        }
-    }
-    std::vector<int> table(G, RAGGED_WT_NONE);
-    for (int x = 0; x < 8; ++x) {
-        std::vector<Job> js = xcd[x];
-        std::stable_sort(js.begin(), js.end(), [](const Job &a, const Job &b) { return a.cost > b.cost; });
-        const int J = (int)js.size(), S = RAGGED_SLOTS;
-        std::vector<Job> order;
-        if (J <= 2 * S || J > 3 * S) {
-            order = js;  // longest first
-        } else {
-            // k3 slots of three (the 3 k3 shortest blocks), the rest in long + short pairs
-            const int k3 = J - 2 * S, nrest = J - 3 * k3;
-            std::vector<std::vector<Job>> q;
-            for (int i = 0; i < nrest / 2; ++i) q.push_back({js[i], js[nrest - 1 - i]});
-            for (int i = 0; i < k3; ++i) q.push_back({js[nrest + 3 * i], js[nrest + 3 * i + 1], js[nrest + 3 * i + 2]});
-            // the dispatch order: every slot's first block, then each slot's next
-            // block at the model time it frees up (ties: slot order)
-            using Ev = std::pair<long, int>;
-            std::vector<size_t> next(q.size(), 1);
-            std::vector<Ev> heap;
-            for (size_t i = 0; i < q.size(); ++i) {
-                order.push_back(q[i][0]);
-                heap.push_back({q[i][0].cost, (int)i});
-            }
-            auto later = [](const Ev &a, const Ev &b) { return a > b; };
-            std::make_heap(heap.begin(), heap.end(), later);
-            while (!heap.empty()) {
-                std::pop_heap(heap.begin(), heap.end(), later);
-                const Ev e = heap.back();
-                heap.pop_back();
-                const int i = e.second;
-                if (next[i] < q[i].size()) {
-                    const Job j = q[i][next[i]++];
-                    order.push_back(j);
-                    heap.push_back({e.first + j.cost, i});
-                    std::push_heap(heap.begin(), heap.end(), later);
-                }
-            }
-        }
-        for (int i = 0; i < J; ++i) table[x * cap + i] = RAGGED_WT(order[i].pair, order[i].qb);
-    }
-    if ((int)tail.size() > G - full) return hipErrorInvalidValue;  // (cannot happen: sum of nb <= G)
-    for (size_t i = 0; i < tail.size(); ++i) table[full + i] = RAGGED_WT(tail[i].pair, tail[i].qb);
-    for (int i0 = 0; i0 < G; i0 += RAGGED_CHUNK) {
-        RaggedChunk c{};
-        const int nb = std::min(RAGGED_CHUNK, G - i0);
-        for (int i = 0; i < nb; ++i) c.n[i] = table[i0 + i];
-        hipLaunchKernelGGL(ragged_order_kernel, dim3(1), dim3(RAGGED_CHUNK), 0, s, c, nb, wt + i0);
-        HIP_RET(hipGetLastError());
-    }
-    return hipSuccess;
-}
-
 }  // namespace pdsc

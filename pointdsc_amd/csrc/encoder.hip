@@ -1523,9 +1523,6 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void pw2_mid_kernel(const floa
 // buffers (Q, K, V, vexp): other workgroups of the pair still read layer l.
 // Bit-identical to attention_h3_kernel + pw2_mid_kernel (a one-split combine
 // is O * (1 / l) exactly).  LDS: the K/V ring, then the weight ring.
-#ifdef PW2_STAGGER
-static __device__ unsigned g_pw2_cu_ctr[16 * 256];
-#endif
 template <bool PACKED>
 __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
@@ -1544,24 +1541,6 @@ __global__ __launch_bounds__(PW2_W * 64, PW2_OCC) void attn_pw2_kernel(
     unsigned long long *stp = att_stamp_ptr(wave);
     ATT_RSTAMP(stp, 188);
     ATT_STAMP(stp, 0);
-#endif
-#ifdef PW2_STAGGER
-    // measurement build (-DPW2_STAGGER=n): the second workgroup to arrive on a CU
-    // starts n x 64 cycles late, so the two workgroups' phases run out of step
-    // (one's chain beside the other's attention) instead of in lockstep.  CU
-    // identity from HW_ID (CU, SH, SE) and XCC_ID; arrival parity from a per-CU
-    // counter (4 workgroups per CU per launch at 128 x 1000 keep it aligned).
-    {
-        __shared__ unsigned stagger_sh;
-        if (tid == 0) {
-            const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);
-            const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
-            stagger_sh = atomicAdd(&g_pw2_cu_ctr[(xcc & 15) * 256 + (hw & 255)], 1u) & 1u;
-        }
-        __syncthreads();
-        if (stagger_sh)
-            for (int i = 0; i < PW2_STAGGER; ++i) __builtin_amdgcn_s_sleep(1);
-    }
 #endif
     f32x16 O[4];
     float m_run, l_run;
@@ -1785,7 +1764,6 @@ hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
-    g.wt = rg.wt;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
     const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
     const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
@@ -1808,7 +1786,6 @@ hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, cons
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
-    g.wt = rg.wt;
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad) return hipErrorInvalidValue;
     W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
     w2_sched_add(S, lay.c0, CH, CLS);

@@ -151,8 +151,6 @@ struct Ragged {
     const int *nv = nullptr, *sv = nullptr;
     // the attention's pair order (longest pairs first, dealt over the XCDs), or null
     const int *po = nullptr;
-    // the fused attention launches' workgroup table (launch_ragged_plan), or null
-    const int *wt = nullptr;
     PDSC_DEV int n(int b, int N) const { return nv ? nv[b] : N; }
     PDSC_DEV int s(int b, int S) const { return sv ? sv[b] : S; }
 };
@@ -165,17 +163,6 @@ hipError_t launch_ragged_setup(const int32_t *counts_host, int B, double ratio, 
 // pairs dealt to the XCD with the least N^2 so far): list scheduling of
 // workgroups of unequal length, longest first
 hipError_t launch_ragged_order(const int32_t *counts_host, int B, int *po, hipStream_t s);
-// counts (HOST) -> wt [B * nqb]: the fused attention launches' workgroups (one
-// per 128-query block of a pair, B * nqb logical ids, nqb = ceil(N / 128)),
-// logical id -> RAGGED_WT(pair, block) or a workgroup with nothing to do
-// (RAGGED_WT_NONE).  Pairs are dealt to the XCDs by work; each XCD's blocks are
-// listed in the order its dispatcher should start them (greedy in-order
-// dispatch to its 2 x 32 slots: longest first paired with shortest, and where
-// the XCD has more than two rounds of blocks, its shortest blocks three to a slot)
-constexpr int RAGGED_WT_QB = 1024;  // block field of a table entry
-#define RAGGED_WT(pair, qb) ((pair) * RAGGED_WT_QB + (qb))
-constexpr int RAGGED_WT_NONE = RAGGED_WT_QB - 1;  // pair 0, block 1023: past every pair's rows
-hipError_t launch_ragged_plan(const int32_t *counts_host, int B, int nqb, int *wt, hipStream_t s);
 
 // ---- launchers --------------------------------------------------------------
 hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const float *sigma_d,

@@ -75,13 +75,13 @@ def main():
         # the gap to the next chunk (epilogues, stores, the next layer's setup)
         ch = []
         for c in range(11):
-            a, b_, e = 192 + 3 * c, 193 + 3 * c, 194 + 3 * c
-            if not (n[:, :, e] > 0).all():
+            i0, i1, i2 = 192 + 3 * c, 193 + 3 * c, 194 + 3 * c
+            if not (n[:, :, i2] > 0).all():
                 break
             nxt = 192 + 3 * (c + 1) if c < 10 and (n[:, :, 192 + 3 * (c + 1)] > 0).all() else 180
-            ch.append({"chunk": c, "mma_us": round(float(us(n[:, :, b_] - n[:, :, a]).mean()), 3),
-                       "sync_us": round(float(us(n[:, :, e] - n[:, :, b_]).mean()), 3),
-                       "after_us": round(float(us(n[:, :, nxt] - n[:, :, e]).mean()), 3)})
+            ch.append({"chunk": c, "mma_us": round(float(us(n[:, :, i1] - n[:, :, i0]).mean()), 3),
+                       "sync_us": round(float(us(n[:, :, i2] - n[:, :, i1]).mean()), 3),
+                       "after_us": round(float(us(n[:, :, nxt] - n[:, :, i2]).mean()), 3)})
         rep["normal"]["chain_chunks"] = ch
     if cfirst.any():
         c = st[cfirst]
