@@ -381,7 +381,7 @@ def main():
             # beats it, the stream-K form (attention_w64_sk_kernel, always 256 workgroups): the
             # committed profile does not record which batch shape a stream-K row is, so no lookup
             flops = P * 4.0 * N * N * 128
-            kname, kdesc, n_launch = None, "attention_w64 (64-query waves, fragment-ordered M; split grid or stream-K)", 12
+            kname, kdesc, n_launch = None, "attention_w64 (64-query waves, symmetric-packed M; split grid or stream-K)", 12
         else:
             flops = P * 4.0 * N * N * 128
             kname, kdesc, n_launch = "attention_h3_kernel<4>", "attention_h3_kernel<4,xcd>", 12
@@ -469,10 +469,7 @@ def main():
             # measured HBM bytes of the same stages from the committed profile (launch
             # shapes as api.hip launches them at this N, P)
             nt5 = (N5 + 63) // 64
-            plan_id = ctypes.c_int32()
-            _lib.check(L.pdsc_encoder_plan(P5, N5, 0, ctypes.byref(plan_id)), "encoder_plan")
-            ck5 = "compat_frag_kernel" if plan_id.value == 2 else "compat_packed_kernel"
-            shapes = [(ck5, nt5 * (nt5 + 1) // 2 * P5 * 256),
+            shapes = [("compat_packed_kernel", nt5 * (nt5 + 1) // 2 * P5 * 256),
                       ("knn_dist_kernel", ((N5 + 31) // 32 + 4) // 5 * ((S5 + 127) // 128) * P5 * 256),
                       ("knn_select_kernel", (S5 + 3) // 4 * P5 * 256),
                       ("nsm_seed_kernel", (S5 + 3) // 4 * P5 * 256), ("nsm_finish_kernel", S5 * P5 * 64)]

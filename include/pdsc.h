@@ -123,15 +123,6 @@ int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N
 size_t pdsc_compat_packed_floats(int32_t N);
 int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                                const float *sigma_d_dev, float *Mp, pdsc_stream_t stream);
-/* The same M in the fragment order the 64-query-wave attention reads (the
- * forward's form where pdsc_encoder_plan reports 2): every 32 x 32 block
- * (query tile qt, key tile kt), nt = ceil(N/32) per side, at float offset
- * (qt*nt + kt)*1024, as 64 lanes x 16 floats: lane l (h = l/32, q = l%32) holds
- * M[32kt + (r%4) + 8(r/4) + 4h][32qt + q] at l*16 + r, r = 0..15; entries past N
- * are 0.  Mf: B * pdsc_compat_frag_floats(N) floats.                         */
-size_t pdsc_compat_frag_floats(int32_t N);
-int32_t pdsc_compat_frag_f32(const float *src, const float *tgt, int32_t B, int32_t N,
-                             const float *sigma_d_dev, float *Mf, pdsc_stream_t stream);
 
 /* -------------------------------------------------- a2-a4 encoder ----------
  * SCNonlocal encoder + F.normalize + classification MLP.
@@ -170,7 +161,7 @@ int32_t pdsc_attention_layout(int32_t B, int32_t N, int32_t precision, int32_t *
  * launch -- these are then the launches pdsc_attention_timing times -- 0
  * when attention and chain are separate launches, and 2 when they are separate
  * and the attention is the 64-query-wave kernel (one 4-wave workgroup per CU,
- * the forward's M in the fragment order of attention_w64.hpp).              */
+ * attention_w64.hpp; the forward's M symmetric-packed as for plans 0/1).    */
 int32_t pdsc_encoder_plan(int32_t B, int32_t N, int32_t precision, int32_t *fused);
 
 /* Measurement hook (bench.py): while capacity > 0, every attention launch the

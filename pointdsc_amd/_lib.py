@@ -66,8 +66,6 @@ _PROTOS = {
     "pdsc_compat_f32": (c_int32, [vp, vp, c_int32, c_int32, vp, vp, vp]),
     "pdsc_compat_packed_floats": (c_size_t, [c_int32]),
     "pdsc_compat_packed_f32": (c_int32, [vp, vp, c_int32, c_int32, vp, vp, vp]),
-    "pdsc_compat_frag_floats": (c_size_t, [c_int32]),
-    "pdsc_compat_frag_f32": (c_int32, [vp, vp, c_int32, c_int32, vp, vp, vp]),
     "pdsc_encoder_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_encoder_f32": (c_int32, [CFG, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_attention_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),

@@ -66,9 +66,8 @@ bool dense_m_requested() {
     return v;
 }
 
-// The forward's M layout: fragment-ordered where the split path runs attention_w64,
-// symmetric-packed for the other H3 plans, dense for exact fp32 (and PDSC_DENSE_M=1
-// on the h3 plans, measurement only).
+// The forward's M layout: symmetric-packed for the H3 plans, dense for exact fp32
+// (and PDSC_DENSE_M=1 on the h3 plans other than attention_w64's, measurement only).
 struct Dims;
 int forward_m_layout(const Dims &d);
 
@@ -104,7 +103,7 @@ struct Dims {
     int B, N, Npad, S, k, T, nsplit;
     bool f32;   // PDSC_PRECISION_F32
     bool fuse;  // attention + pointwise chain in one launch per layer (attention_fused)
-    bool w64;   // split path with attention_w64 (fragment-ordered M)
+    bool w64;   // split path with attention_w64 (64-query waves)
     bool precombine;  // split partials combined by combine_rows ahead of the pointwise kernels
 };
 
@@ -128,7 +127,7 @@ int make_dims(const pdsc_config *cfg, int B, int N, Dims &d) {
 }
 
 int forward_m_layout(const Dims &d) {
-    if (d.w64) return M_FRAG;
+    if (d.w64) return M_PACKED;
     return (!dense_m_requested() && !d.f32) ? M_PACKED : M_DENSE;
 }
 
@@ -172,7 +171,8 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                 int m_layout, const Dims &d, const EncBufs &e, float *feat_out, float *normed,
                 _Float16 *normed_s, float *conf, hipStream_t s, Ragged rg = {}) {
     const bool m_packed = m_layout == M_PACKED;
-    if ((m_layout == M_FRAG) != (d.w64 && !d.fuse)) return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
+    const bool w64 = d.w64 && !d.fuse;
+    if (w64 && m_layout != M_PACKED) return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
     HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg));
     if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
@@ -196,8 +196,8 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
     for (int l = 0; l < lay.L; ++l) {
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
-        HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_layout, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart, e.ml,
-                                s, rg));
+        HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_layout, w64, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart,
+                                e.ml, s, rg));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         const float *op = e.opart, *mlp = e.ml;
         int ns = d.nsplit;
@@ -274,7 +274,7 @@ FwdBufs carve_forward(Carve &c, const Dims &d) {
     FwdBufs f;
     f.range = c.take<int>((size_t)d.B);  // first: at the workspace's base
     // symmetric-packed tiles (PDSC_DENSE_M=1: the dense [N][N] form, for A/B measurement)
-    f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), mfrag_floats(d.N)));  // (mfrag >= N^2: dense fits)
+    f.M = c.take<float>((size_t)d.B * std::max(mpack_floats(d.N), (size_t)d.N * d.N));  // packed or dense
     f.enc = carve_encoder(c, d);
     f.normed = c.take<float>((size_t)d.B * d.N * CH);
     f.normed_s = c.take<_Float16>((size_t)d.B * d.N * 2 * CH);
@@ -415,15 +415,6 @@ int32_t pdsc_compat_f32(const float *src, const float *tgt, int32_t B, int32_t N
 }
 
 size_t pdsc_compat_packed_floats(int32_t N) { return N < 1 ? 0 : mpack_floats(N); }
-size_t pdsc_compat_frag_floats(int32_t N) { return N < 1 ? 0 : mfrag_floats(N); }
-
-int32_t pdsc_compat_frag_f32(const float *src, const float *tgt, int32_t B, int32_t N, const float *sigma_d_dev,
-                             float *Mf, pdsc_stream_t stream) {
-    if (!src || !tgt || !sigma_d_dev || !Mf) return fail(PDSC_ERR_ARG, "null pointer");
-    if (B < 1 || N < 1) return fail(PDSC_ERR_ARG, "B=%d N=%d", B, N);
-    HIPCHK(launch_compat_frag(src, tgt, B, N, sigma_d_dev, Mf, S_(stream)));
-    return PDSC_OK;
-}
 
 int32_t pdsc_compat_packed_f32(const float *src, const float *tgt, int32_t B, int32_t N,
                                const float *sigma_d_dev, float *Mp, pdsc_stream_t stream) {
@@ -502,7 +493,7 @@ int32_t pdsc_attention_f32(const float *q, const float *k, const float *v, const
     } else {  // the caller's fp32 [B][N][C] rows -> the kernel's padded fp16 hi/lo layouts
         HIPCHK(launch_split_qkv(q, k, v, B, N, N, Npad, qs, ks, vs, vexp, s));
     }
-    HIPCHK(launch_attention(qs, ks, vs, vexp, M, M_DENSE, f32, B, N, Npad, ns, op, ml, s));
+    HIPCHK(launch_attention(qs, ks, vs, vexp, M, M_DENSE, false, f32, B, N, Npad, ns, op, ml, s));
     HIPCHK(launch_attn_combine(op, ml, f32, B, N, Npad, ns, msg, s));
     return PDSC_OK;
 }
@@ -730,9 +721,7 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     // launch measured no gain at 128 x 1000 / 8 x 5000 and +44 us per single
     // pair -- the cross-stream event pair -- so the forward stays on one stream.)
     const int mlay = forward_m_layout(d);
-    if (mlay == M_FRAG)
-        HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
-    else if (mlay == M_PACKED)
+    if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
@@ -811,9 +800,7 @@ int32_t pdsc_forward_training(const pdsc_config *cfg, const float *packed, const
     const float *sigma = packed + lay.sigma, *sigma_d = packed + lay.sigma_d;
     // a1-a4 as in testing (:150-156, :171)
     const int mlay = forward_m_layout(d);
-    if (mlay == M_FRAG)
-        HIPCHK(launch_compat_frag(src, tgt, d.B, d.N, sigma_d, f.M, s));
-    else if (mlay == M_PACKED)
+    if (mlay == M_PACKED)
         HIPCHK(launch_compat_packed(src, tgt, d.B, d.N, sigma_d, f.M, s));
     else
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s));

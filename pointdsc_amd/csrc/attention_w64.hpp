@@ -114,21 +114,55 @@ template <int A> PDSC_DEV float w64_read_a() {
     asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(A));
     return x;
 }
-// 16 B of M at voff of resource r, by asm: hipcc does not count it, so its wait
-// is the kernel's own (w64_mwait) and never merges with the DMA bookkeeping
-PDSC_DEV f32x4 w64_mload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-    f32x4 x;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(x) : "v"(voff), "s"(r) : "memory");
-    return x;
+// ---- M, asm-owned VGPRs -------------------------------------------------------
+// The two M register sets (tile t's and tile t + 1's, both blocks) live in
+// v[192:255]: set s, block u at v[W64_VM + 32 s + 16 u .. + 15], register r =
+// this lane's M[32 kt + acc_row(r, h)][32 qt + l32].  hipcc is capped below them
+// (amdgpu_num_vgpr) and never sees them: the loads, their waits and the two
+// softmax instructions that read them are asm, so the register-to-load binding
+// cannot be broken by a copy or a reuse while a load is in flight, and the two
+// load shapes below (one of them four 4-byte ops) fill the same registers.
+constexpr int W64_VM = 192;
+PDSC_DEV void w64_claim_vm() {
+    asm volatile("" ::: "v192","v193","v194","v195","v196","v197","v198","v199","v200","v201","v202","v203","v204","v205","v206","v207","v208","v209","v210","v211","v212","v213","v214","v215","v216","v217","v218","v219","v220","v221","v222","v223","v224","v225","v226","v227","v228","v229","v230","v231","v232","v233","v234","v235","v236","v237","v238","v239","v240","v241","v242","v243","v244","v245","v246","v247","v248","v249","v250","v251","v252","v253","v254","v255");
 }
-// all but the N youngest vector-memory ops done; the 8 M quads now readable
-template <int N> PDSC_DEV void w64_mwait(f32x4 (&m)[2][4]) {
-    asm volatile("s_waitcnt vmcnt(%8)"
-                 : "+v"(m[0][0]), "+v"(m[0][1]), "+v"(m[0][2]), "+v"(m[0][3]), "+v"(m[1][0]), "+v"(m[1][1]),
-                   "+v"(m[1][2]), "+v"(m[1][3])
-                 : "n"(N)
+// M quad G (registers R + 4 G ..) of a lane from the symmetric-packed layout
+// (row-major 32 x 32 tiles, pdsc_internal.hpp mpack_tile).  Rows = queries (tile
+// (qt, kt), kt > qt): 16 B of the lane's row, one op.  Rows = keys (tile (kt,
+// qt), kt <= qt): 4 words of the lane's column 128 B apart, four ops (each a
+// coalesced 128-B row piece per half-wave).  hipcc does not count these loads:
+// their waits are the kernel's own.
+template <int R, int G> PDSC_DEV void w64_mload_row(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    asm volatile("buffer_load_dwordx4 v[%c0:%c1], %2, %3, 0 offen offset:%c4" ::"i"(R + 4 * G), "i"(R + 4 * G + 3),
+                 "v"(voff), "s"(r), "i"(32 * G)
                  : "memory");
 }
+template <int R, int G> PDSC_DEV void w64_mload_col(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    asm volatile("buffer_load_dword v%c0, %4, %5, 0 offen offset:%c6\n\t"
+                 "buffer_load_dword v%c1, %4, %5, 0 offen offset:%c7\n\t"
+                 "buffer_load_dword v%c2, %4, %5, 0 offen offset:%c8\n\t"
+                 "buffer_load_dword v%c3, %4, %5, 0 offen offset:%c9" ::"i"(R + 4 * G), "i"(R + 4 * G + 1),
+                 "i"(R + 4 * G + 2), "i"(R + 4 * G + 3), "v"(voff), "s"(r), "i"(1024 * G), "i"(1024 * G + 128),
+                 "i"(1024 * G + 256), "i"(1024 * G + 384)
+                 : "memory");
+}
+// all but the N youngest vector-memory ops done
+template <int N> PDSC_DEV void w64_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// a block's M ready: 8 + (4 or 16) younger ops -- the DMA pieces around the
+// other block's M, whose op count depends on its orientation (scalar branch)
+PDSC_DEV void w64_mwait_after(bool other_keyrows) {
+    if (other_keyrows)
+        w64_vmwait<8 + 16>();
+    else
+        w64_vmwait<8 + 4>();
+}
+// p = M[r] s - mb (softmax part 1), p = M[r] p (the first tile)
+template <int R> PDSC_DEV float w64_fma_m(float sv, float mb) {
+    float p;
+    asm volatile("v_fma_f32 %0, v%c1, %2, -%3" : "=v"(p) : "i"(R), "v"(sv), "v"(mb));
+    return p;
+}
+template <int R> PDSC_DEV void w64_mul_m(float &p) { asm volatile("v_mul_f32 %0, v%c1, %0" : "+v"(p) : "i"(R)); }
 
 // Diagnostic build only (-DW64_STAMPS, tools/att_w64_bench.hip): s_memtime at
 // region boundaries of every tile, kept in LDS past W64_LDS (no vector-memory
@@ -154,10 +188,6 @@ constexpr size_t W64_ST_LDS = 0;
     } while (0)
 #endif
 
-// block u's 4 M quads ready (all but the N youngest vector-memory ops done)
-template <int N> PDSC_DEV void w64_mwait_blk(f32x4 (&m)[4]) {
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]) : "n"(N) : "memory");
-}
 // split2 (attention_h3.hpp) as three single-instruction statements, so a
 // softmax slice carries one of them: hi = {f16(x0), f16(x1)}, then lo's halves
 // by v_fma_mixlo / v_fma_mixhi (x - hi exact, one rounding).  No s_nop: the P
@@ -209,7 +239,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     const char *Kp = reinterpret_cast<const char *>(Ks + (size_t)b * Npad * 2 * CH);
     const char *Vp = reinterpret_cast<const char *>(Vs + (size_t)b * Npad * 2 * CH);
     const int mnt = mpack_ntile(g.N);  // M's layout is the batch stride's
-    const size_t mper = mfrag_floats(g.N);
+    const size_t mper = mpack_floats(g.N);
 #ifdef W64_EXP_MSHARED  // diagnostic: every pair reads pair 0's M (L2 / MALL resident)
     const __amdgpu_buffer_rsrc_t rM = h3_rsrc(M, (uint32_t)(mper * 4u));
 #else
@@ -223,6 +253,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     w64_claim_agprs();
+    w64_claim_vm();
     static_for<128>([&](auto ic) { w64_zero_a<W64_AO + decltype(ic)::value>(); });
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -261,10 +292,41 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void *)dst, 16, 16 * lane,
                                                  st * H3_KTB + (pbase + i) * 1024, 0, 0);
     };
-    // M of tile st, block u, quad gg (mfrag_off: this lane's 16 values
-    // contiguous; 1 KiB contiguous per wave instruction) and the V exponent
-    auto load_mq = [&](int st, int u, int gg) {  // (qt past the layout: zeros)
-        return w64_mload(rM, (uint32_t)(mfrag_off((q0 >> 5) + u, st, mnt) * 4) + 64u * lane + 16u * gg);
+    // M of tile st, block u, quad gg: this lane's 16 values M[32 st + acc_row(r, h)]
+    // [32 qt + l32] from packed tile (st, qt) (rows = keys: column l32, rows 4 h +
+    // 8 gg ..) or (qt, st) (rows = queries: row l32, columns 4 h + 8 gg ..).  The
+    // offsets of attention_h3_core's packed loads (a block past the layout reads
+    // past the resource: zeros).
+    const int qt0 = q0 >> 5;  // block A's query tile (wave-uniform)
+    const uint32_t vcol = (uint32_t)(4 * h * MPACK_T + (lane & 31)) * 4u;
+    const uint32_t vrow = (uint32_t)((lane & 31) * MPACK_T + 4 * h) * 4u;
+    auto keyrows = [&](int st, int u) { return st <= qt0 + u; };  // tile st of block u is read by columns
+    // the load shape of tile st, block u under a tile step's shape SH: 1 = every
+    // block by columns (st <= qt0), 2 = every block by rows (st > qt0 + 1),
+    // 0 = per block at run time.  The key tiles of a query block run through
+    // shape 1, one or two mixed steps, then shape 2: the kernel's tile steps
+    // come in those three compiled forms, so the hot loops carry no per-load
+    // branch (per-load scalar branches measured 300 vs 274 us per launch).
+    auto kr = [&](auto shc, int st, int u) {
+        constexpr int SH = decltype(shc)::value;
+        if constexpr (SH == 1)
+            return true;
+        else if constexpr (SH == 2)
+            return false;
+        else
+            return keyrows(st, u);
+    };
+    using SH0 = std::integral_constant<int, 0>;
+    using SH1 = std::integral_constant<int, 1>;
+    using SH2 = std::integral_constant<int, 2>;
+    // quad gg of block u's M of tile st into register set ms
+    auto load_mq = [&](auto shc, auto msc, auto uc, auto gc, int st) {
+        constexpr int R = W64_VM + 32 * decltype(msc)::value + 16 * decltype(uc)::value, gg = decltype(gc)::value;
+        const int qt = qt0 + decltype(uc)::value;
+        if (kr(shc, st, decltype(uc)::value))
+            w64_mload_col<R, gg>(rM, vcol + (uint32_t)mpack_tile(st, qt, mnt) * (MPACK_T * MPACK_T * 4u));
+        else
+            w64_mload_row<R, gg>(rM, vrow + (uint32_t)mpack_tile(qt, st, mnt) * (MPACK_T * MPACK_T * 4u));
     };
     const float *ev_lds = reinterpret_cast<const float *>(smem + W64_RING);
     auto load_ev = [&](int st) { return ev_lds[st]; };  // (wave-uniform address: one broadcast read)
@@ -296,8 +358,8 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     // softmax part 1, slice k (0 .. 23) of block u (tile key0, its M and ev):
     // p = M S - base (one fma), the tile's max, the re-base test (attention_h3_core
     // arithmetic, not the first tile)
-    auto sm1_slice = [&](auto kc, int u, const f32x16 &S, const f32x4 (&mv)[4], float ev, int key0, SmA &a) {
-        constexpr int k = decltype(kc)::value;
+    auto sm1_slice = [&](auto kc, int u, const f32x16 &S, auto mrc, float ev, int key0, SmA &a) {
+        constexpr int k = decltype(kc)::value, MR = decltype(mrc)::value;  // MR: the block's M registers
 #ifdef W64_EXP_NO_SM1  // diagnostic: no part-1 VALU (p = S)
         if constexpr (k >= 1 && k <= 16) a.p[k - 1] = S[k - 1];
         if constexpr (k == 22) a.resc = false;
@@ -309,7 +371,7 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
             w64_pin(a.mb0);
         } else if constexpr (k <= 16) {
             constexpr int r = k - 1;
-            a.p[r] = __builtin_fmaf(mv[r >> 2][r & 3], S[r], -a.mb0);
+            a.p[r] = w64_fma_m<MR + r>(S[r], a.mb0);
             w64_pin(a.p[r]);
         } else if constexpr (k <= 20) {
             if constexpr (k == 17) {
@@ -345,13 +407,13 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         }
     };
     // the first tile's part 1 (m_run = -inf, O = 0: attention_h3_core's first-tile arithmetic)
-    auto sm1_first = [&](int u, const f32x16 &S, const f32x4 (&mv)[4], float ev, int key0, SmA &a) {
+    auto sm1_first = [&](int u, const f32x16 &S, auto mrc, float ev, int key0, SmA &a) {
+        constexpr int MR = decltype(mrc)::value;
         const float scale = ATT_QFMA ? 1.0f : H3_QSCALE;
         float mx = -INFINITY;
 #pragma unroll
         for (int r = 0; r < 16; ++r) a.p[r] = S[r] * scale;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a.p[r] = mv[r >> 2][r & 3] * a.p[r];
+        static_for<16>([&](auto rc) { w64_mul_m<MR + decltype(rc)::value>(a.p[decltype(rc)::value]); });
         if (key0 + 32 > N) {
 #pragma unroll
             for (int r = 0; r < 16; ++r)
@@ -490,28 +552,35 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     auto none = [](auto) {};
 
     // end of R3: tile t + 1's DMA (issued in R2 and R4 of tile t - 1) has landed;
-    // younger than it: R2(t)'s 4 M quads and 4 DMA pieces.  vmcnt(8), no lgkm / exp wait.
-    auto mid_barrier = [&] {
-        __builtin_amdgcn_s_waitcnt(0x0F78);
+    // younger than it: R2(t)'s block A M ops (of tile tn) and 4 DMA pieces.
+    // vmcnt(8) or vmcnt(20), no lgkm / exp wait.
+    auto mid_barrier = [&](auto shc, int tn) {
+        if (kr(shc, tn, 0))
+            __builtin_amdgcn_s_waitcnt(0x4F74);  // vmcnt(20) = 16 + 4
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8) = 4 + 4
         __builtin_amdgcn_s_barrier();
     };
 
-    f32x4 mX[2][4], mY[2][4];
+    using MSX = std::integral_constant<int, 0>;  // the M register sets
+    using MSY = std::integral_constant<int, 1>;
+    auto mregs = [](auto msc, auto uc) { return std::integral_constant<int, W64_VM + 32 * decltype(msc)::value + 16 * decltype(uc)::value>{}; };
     float eX, eY;
     f32x16 S[2];
     SmA sa[2];
     SmB sb;
     f16x8 ph[2][2], pl[2][2];
 
-    // The vector-memory issue of a tile, one op per 3 MFMAs: in R2 block A's 4 M
-    // quads of tile tn and DMA pieces 0-3 of tile td, in R4 block B's quads and
-    // pieces 4-7 (slices 1, 4, 7, 10: M; 13, 16, 19, 22: DMA).  Static counts:
-    // a block's M wait finds 12 younger ops (its half's 4 pieces, the other
-    // half's 8), the barrier 8 (R2's).
-    auto issue_half = [&](auto kc, auto hc, int tn, int td, f32x4 (&mn)[2][4]) {
+    // The vector-memory issue of a tile, one M quad (1 or 4 ops) or DMA piece
+    // per 3 MFMAs: in R2 block A's 4 M quads of tile tn and DMA pieces 0-3 of
+    // tile td, in R4 block B's quads and pieces 4-7 (slices 1, 4, 7, 10: M; 13,
+    // 16, 19, 22: DMA).  A block's M wait finds 8 + (the other block's M ops)
+    // younger ops (its half's 4 pieces, the other half's M and 4 pieces), the
+    // barrier 4 + (R2's M ops).
+    auto issue_half = [&](auto shc, auto kc, auto hc, int tn, int td, auto msn) {
         constexpr int k = decltype(kc)::value, half = decltype(hc)::value;
 #ifndef W64_EXP_NO_M
-        if constexpr (k % 3 == 1 && k <= 10) mn[half][k / 3] = load_mq(tn, half, k / 3);
+        if constexpr (k % 3 == 1 && k <= 10) load_mq(shc, msn, hc, std::integral_constant<int, k / 3>{}, tn);
 #endif
 #ifndef W64_EXP_NO_DMA
         if constexpr (k % 3 == 1 && k >= 13) stage_piece(td, 4 * half + (k - 13) / 3);
@@ -525,15 +594,12 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
     for (int i = 0; i < DMA_PW; ++i) stage_piece(st0, i);
 #pragma unroll
     for (int i = 0; i < DMA_PW; ++i) stage_piece(st0 + 1, i);
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) mX[u][gg] = load_mq(st0, u, gg);
+    static_for<2>([&](auto uc) { static_for<4>([&](auto gc) { load_mq(SH0{}, MSX{}, uc, gc, st0); }); });
     {
         float *evw = reinterpret_cast<float *>(smem + W64_RING);
         for (int i = threadIdx.x; i < Npad / H3_TILE; i += W64_NW * 64) evw[i] = vexp_b[i];
     }
-    w64_mwait<0>(mX);  // (the Q and M loads are asm: hipcc does not count them)
+    w64_vmwait<0>();  // (the Q and M loads are asm: hipcc does not count them)
     __builtin_amdgcn_s_waitcnt(0x0070);               // vmcnt(0) lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     eX = load_ev(st0);
@@ -547,22 +613,22 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         // R1: QK_A
         qk_region(std::integral_constant<int, 0>{}, L, S[0], none, none);
         // R2: softmax_A part 1 (first tile) + the issue of tile t + 1's M and tile t + 2's DMA
-        static_for<24>([&](auto kc) { issue_half(kc, H0{}, min(t + 1, st1 - 1), t + 2, mY); });
+        static_for<24>([&](auto kc) { issue_half(SH0{}, kc, H0{}, min(t + 1, st1 - 1), t + 2, MSY{}); });
         eY = load_ev(min(t + 1, st1 - 1));
         kread(L, 0, kf.f[0]);  // (QK_A's last k-steps held kf[0], kf[1]: R3's first two only now)
         kread(L, 1, kf.f[1]);
-        sm1_first(0, S[0], mX[0], eX, key0, sa[0]);
+        sm1_first(0, S[0], mregs(MSX{}, H0{}), eX, key0, sa[0]);
         // R3: QK_B + softmax_A part 2
         qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(L + H3_KTB),
                   [&](auto kc) { sm2_slice(kc, 0, sa[0], eX, sb, ph[0], pl[0]); });
-        mid_barrier();
+        mid_barrier(SH0{}, min(t + 1, st1 - 1));
         // R4: PV_A + softmax_B part 1 (first tile)
         pv_region(std::integral_constant<int, 0>{}, L + H3_KTB, ph[0], pl[0], next_k(slot_of(t + 1)),
-                  [&](auto kc) { issue_half(kc, H1{}, min(t + 1, st1 - 1), t + 2, mY); });
-        sm1_first(1, S[1], mX[1], eX, key0, sa[1]);
+                  [&](auto kc) { issue_half(SH0{}, kc, H1{}, min(t + 1, st1 - 1), t + 2, MSY{}); });
+        sm1_first(1, S[1], mregs(MSX{}, H1{}), eX, key0, sa[1]);
     }
     // ---- steady state: tile t (its M in mc, ev ec; the next tile's into mn, en) ----
-    auto tile = [&](int t, f32x4 (&mc)[2][4], float &ec, float &ep, f32x4 (&mn)[2][4], float &en) {
+    auto tile = [&](int t, auto msc, float &ec, float &ep, auto msn, float &en, auto shc) {
         const int key0 = t * H3_TILE;
         const int si = W64_ST_PER_TILE * min(t - st0, 39);
         (void)si;
@@ -574,11 +640,11 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         W64_ST(si + 1);
         // R2: PV_B(t - 1) + softmax_A(t) part 1 + tile t + 1's M, tile t + 2's DMA
         pv_region(std::integral_constant<int, 1>{}, Lp + H3_KTB, ph[1], pl[1], next_k(L), [&](auto kc) {
-            // block A's M of tile t (issued in R2 of tile t - 1; 12 younger ops)
-            if constexpr (decltype(kc)::value == 0) w64_mwait_blk<12>(mc[0]);
+            // block A's M of tile t (issued in R2 of tile t - 1; younger: 8 + block B's)
+            if constexpr (decltype(kc)::value == 0) w64_mwait_after(kr(shc, t, 1));
             if constexpr (decltype(kc)::value == 2) en = load_ev(min(t + 1, st1 - 1));
-            sm1_slice(kc, 0, S[0], mc[0], ec, key0, sa[0]);
-            issue_half(kc, H0{}, min(t + 1, st1 - 1), t + 2, mn);
+            sm1_slice(kc, 0, S[0], mregs(msc, H0{}), ec, key0, sa[0]);
+            issue_half(shc, kc, H0{}, min(t + 1, st1 - 1), t + 2, msn);
         });
         rebase(std::integral_constant<int, 0>{}, sa[0]);
         W64_ST(si + 2);
@@ -586,14 +652,15 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
         qk_region(std::integral_constant<int, 1>{}, L, S[1], next_v(L + H3_KTB),
                   [&](auto kc) { sm2_slice(kc, 0, sa[0], ec, sb, ph[0], pl[0]); });
         W64_ST(si + 3);
-        mid_barrier();
+        mid_barrier(shc, min(t + 1, st1 - 1));
         W64_ST(si + 4);
         // R4: PV_A(t) + softmax_B(t) part 1
         pv_region(std::integral_constant<int, 0>{}, L + H3_KTB, ph[0], pl[0], next_k(slot_of(t + 1)), [&](auto kc) {
-            // block B's M of tile t (issued in R4 of tile t - 1; 12 younger ops)
-            if constexpr (decltype(kc)::value == 0) w64_mwait_blk<12>(mc[1]);
-            sm1_slice(kc, 1, S[1], mc[1], ec, key0, sa[1]);
-            issue_half(kc, H1{}, min(t + 1, st1 - 1), t + 2, mn);
+            // block B's M of tile t (issued in R4 of tile t - 1; younger: 8 + block A's
+            // of tile t + 1, issued in R2)
+            if constexpr (decltype(kc)::value == 0) w64_mwait_after(kr(shc, min(t + 1, st1 - 1), 0));
+            sm1_slice(kc, 1, S[1], mregs(msc, H1{}), ec, key0, sa[1]);
+            issue_half(shc, kc, H1{}, min(t + 1, st1 - 1), t + 2, msn);
         });
         rebase(std::integral_constant<int, 1>{}, sa[1]);
         W64_ST(si + 5);
@@ -603,21 +670,32 @@ PDSC_DEV void attention_w64_core(const _Float16 *__restrict__ Qs, const _Float16
 #endif
     int t = st0 + 1;
     for (; t + 1 < st1; t += 2) {
-        tile(t, mY, eY, eX, mX, eX);
-        tile(t + 1, mX, eX, eY, mY, eY);
+        // the step's shape (see kr): 1 if its next tile's M are by columns for
+        // both blocks (then so is the current tile's block B), 2 if the current
+        // tile is past both blocks' query tiles
+        auto shape = [&](int tt) { return min(tt + 1, st1 - 1) <= qt0 ? 1 : (tt >= qt0 + 2 ? 2 : 0); };
+        const int s0 = shape(t), s1 = shape(t + 1);
+        auto two = [&](auto shc) {
+            tile(t, MSY{}, eY, eX, MSX{}, eX, shc);
+            tile(t + 1, MSX{}, eX, eY, MSY{}, eY, shc);
+        };
+        if (s0 == 1 && s1 == 1)
+            two(SH1{});
+        else if (s0 == 2 && s1 == 2)
+            two(SH2{});
+        else
+            two(SH0{});
     }
     // (ep of the pair's first tile above: eX before it is overwritten in R2 --
     // part 2 of block B reads it in R1, ahead of the loads)
     if (t < st1) {
-        tile(t, mY, eY, eX, mX, eX);
+        tile(t, MSY{}, eY, eX, MSX{}, eX, SH0{});
         ++t;
     }
     // ---- epilogue: softmax_B(last) part 2, PV_B(last) ----
-    // The last tile loaded a "next" M that nothing reads: its registers must stay
-    // allocated until the asm loads have landed (hipcc would otherwise hand them
-    // to the V fragments below, and the late loads would overwrite those).
-    w64_mwait<0>(mX);
-    w64_mwait<0>(mY);
+    // The last tile loaded a "next" M that nothing reads: landed before the
+    // core returns (the registers are the next segment's).
+    w64_vmwait<0>();
     {
         const float el = ((t - st0) & 1) ? eX : eY;  // the last tile's exponent
         const char *Lp = slot_of(t - 1);
@@ -688,7 +766,7 @@ PDSC_DEV void w64_store_partial(const AttnGridH3 &g, const AttnBlock &blk, float
 
 // Split-K attention with 64-query waves: partials as attention_h3_kernel.
 template <bool XCD>
-__global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_kernel(
+__global__ __launch_bounds__(W64_NW * 64, 1) __attribute__((amdgpu_num_vgpr(W64_VM))) void attention_w64_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
     float *__restrict__ ml) {
@@ -736,7 +814,7 @@ PDSC_DEV void w64_zero_partial(const AttnGridH3 &g, int b, int qb, int s, float 
 }
 
 template <bool XCD>
-__global__ __launch_bounds__(W64_NW * 64, 1) void attention_w64_sk_kernel(
+__global__ __launch_bounds__(W64_NW * 64, 1) __attribute__((amdgpu_num_vgpr(W64_VM))) void attention_w64_sk_kernel(
     const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
     const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, int nwg, float *__restrict__ opart,
     float *__restrict__ ml) {

@@ -260,111 +260,6 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
     }
 }
 
-// The h3 forward's M in the fragment order of attention_w64 (pdsc_internal.hpp,
-// mfrag_off): each 32 x 32 block (query tile qt, key tile kt) as 64 lanes x 16
-// floats, lane (h, q) holding M[32 kt + acc_row(r, h)][32 qt + q].  A workgroup
-// computes a 64 x 64 upper-triangle block once (compat4, as compat_packed_kernel),
-// stages it in LDS, and stores each of its 32 x 32 tiles in both roles (the
-// transposed one from the same LDS image): every block 4 contiguous 1-KiB wave
-// stores.  The dense matrix's bytes (4 N^2 per pair, twice the packed form) buy
-// the attention one load shape for every block (4 x 16 B per lane, 1 KiB
-// contiguous per wave instruction).  Entries past N are written as 0.
-__global__ __launch_bounds__(256) void compat_frag_kernel(const float *__restrict__ src, const float *__restrict__ tgt,
-                                                          int Nstr, int ntile, const float *__restrict__ sigma_d_ptr,
-                                                          float *__restrict__ Mf, Ragged rg) {
-    __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
-    __shared__ CompatScratch scr[4];
-    __shared__ float T[CT][CT + 1];  // the 64 x 64 block, rows i, columns j
-    int t = blockIdx.x, ti = 0;
-    while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
-    const int tj = ti + t;
-    const int b = blockIdx.y;
-    const int N = rg.n(b, Nstr);
-    if (ti * CT >= N) return;  // workgroup-uniform (no wave of this pair reads those blocks' valid rows)
-    const float sd = sigma_d_ptr[0];
-    const float s2 = sd * sd;
-    const float rs2 = 1.0f / s2;
-    const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
-    const float kzero = 2.0f * s2 * (1.0f + 0x1p-10f), gmax = 0x1p20f * s2;  // compat4's zero test
-    src += (size_t)b * Nstr * 3;
-    tgt += (size_t)b * Nstr * 3;
-    const int nt32 = mpack_ntile(Nstr);
-    float *Mb = Mf + (size_t)b * mfrag_floats(Nstr);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int i0 = ti * CT, j0 = tj * CT;
-    for (int e = tid; e < CT * 3; e += 256) {
-        const int p = e / 3, c = e % 3;
-        pts[0][p][c] = (i0 + p < N) ? src[(size_t)(i0 + p) * 3 + c] : 0.f;
-        pts[1][p][c] = (i0 + p < N) ? tgt[(size_t)(i0 + p) * 3 + c] : 0.f;
-        pts[2][p][c] = (j0 + p < N) ? src[(size_t)(j0 + p) * 3 + c] : 0.f;
-        pts[3][p][c] = (j0 + p < N) ? tgt[(size_t)(j0 + p) * 3 + c] : 0.f;
-    }
-    __syncthreads();
-    const int cq = tid & 15, rq = tid >> 4;
-    const int tc = 2 * tj + (cq >> 3);
-    float cs[4][3], ct[4][3];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            cs[q][k] = pts[2][cq * 4 + q][k];
-            ct[q][k] = pts[3][cq * 4 + q][k];
-        }
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int r = rq + 16 * rr;
-        const int tr = 2 * ti + (r >> 5);
-        // below the diagonal (diagonal block) / past the layout: not needed
-        const bool skip = tr > tc || tr >= nt32 || tc >= nt32;
-        if (__all(skip)) continue;  // wave-uniform
-        const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
-        const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
-        float xs[4], xt[4], out[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            xs[q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
-            xt[q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
-        }
-        compat4(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) T[r][cq * 4 + q] = (i0 + r >= N || j0 + cq * 4 + q >= N) ? 0.0f : out[q];
-    }
-    __syncthreads();
-    // 32 x 32 tiles (sr, sc) of the block with tr <= tc: block (qt = tc, kt = tr)
-    // (keys = rows i) and, off the diagonal, block (qt = tr, kt = tc) (keys =
-    // columns j).  Wave w stores the blocks w and w + 4 of these 8 roles; store g
-    // of a block: lane L writes block-lane 16 g + L / 4's registers 4 (L % 4) .. + 3
-    // = 4 consecutive keys e + 8 c + 4 h of its query.
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int role = wave + 4 * k;  // (sr, sc) = role & 3, transposed = role >> 2
-        const int sr = (role >> 1) & 1, sc = role & 1, tpos = role >> 2;
-        const int tr = 2 * ti + sr, tcc = 2 * tj + sc;
-        if (tr > tcc || tr >= nt32 || tcc >= nt32 || (tpos && tr == tcc)) continue;  // wave-uniform
-        const int qt = tpos ? tr : tcc, kt = tpos ? tcc : tr;
-        float *blk = Mb + mfrag_off(qt, kt, nt32);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int bl = 16 * g + (lane >> 2), c = lane & 3, hh = bl >> 5, q = bl & 31;
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int key = e + 8 * c + 4 * hh;
-                v[e] = tpos ? T[32 * sr + q][32 * sc + key] : T[32 * sr + key][32 * sc + q];
-            }
-            *reinterpret_cast<f32x4 *>(blk + 256 * g + 4 * lane) = f32x4{v[0], v[1], v[2], v[3]};
-        }
-    }
-}
-
-hipError_t launch_compat_frag(const float *src, const float *tgt, int B, int N, const float *sigma_d, float *Mf,
-                              hipStream_t stream, Ragged rg) {
-    const int ntile = (N + CT - 1) / CT;
-    const int ntri = ntile * (ntile + 1) / 2;
-    hipLaunchKernelGGL(compat_frag_kernel, dim3(ntri, B), dim3(256), 0, stream, src, tgt, N, ntile, sigma_d, Mf, rg);
-    return hipGetLastError();
-}
-
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
                                 float *Mp, hipStream_t stream, Ragged rg) {
     const int ntile = (N + CT - 1) / CT;  // 64-point compute blocks

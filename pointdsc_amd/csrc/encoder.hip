@@ -147,7 +147,7 @@ constexpr int ATT_F32_KTS = 32;
 static AttnGrid f32_grid(int B, int N) { return attention_grid<ATT_NW, ATT_F32_KTS>(B, N, att_target()); }
 
 // The 64-query-wave attention (attention_w64.hpp, one 4-wave workgroup per CU,
-// fragment-ordered M) for the split path: from 128 blocks of 256 queries
+// symmetric-packed M) for the split path: from 128 blocks of 256 queries
 // (8 x 5000: 160 blocks, 3 key splits).  Knob PDSC_W64: 0 never, 1 wherever the
 // split path runs (measurement only).
 static AttnGridH3 w64_grid(int B, int N) { return attention_w64_grid(B, N, att_target() / 2); }
@@ -188,11 +188,11 @@ int attention_nsplit(int B, int N, bool f32, bool w64) {
 }
 
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
-                            int m_layout, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
-                            hipStream_t s, Ragged rg) {
+                            int m_layout, bool w64, bool f32, int B, int N, int Npad, int nsplit, float *opart,
+                            float *ml, hipStream_t s, Ragged rg) {
     const bool m_packed = m_layout == M_PACKED;
-    if (m_layout == M_FRAG) {  // attention_w64 (H3 layouts, fragment-ordered M)
-        if (f32) return hipErrorInvalidValue;
+    if (w64) {  // attention_w64 (H3 layouts, symmetric-packed M)
+        if (f32 || !m_packed) return hipErrorInvalidValue;
         AttnGridH3 g = w64_grid(B, N);
         if (g.Npad != Npad || nsplit != w64_nsplit(B, N)) return hipErrorInvalidValue;
         g.nsplit = nsplit;  // slots past the split grid's own: empty splits (st0 >= st1)

@@ -28,17 +28,6 @@ __host__ __device__ inline size_t mpack_floats(int N) {
     return nt * (nt + 1) / 2 * MPACK_T * MPACK_T;
 }
 __host__ __device__ inline int mpack_tile(int ti, int tj, int nt) { return ti * nt - ti * (ti - 1) / 2 + (tj - ti); }
-// ---- fragment-ordered M (the h3 forward's a1 output, attention_w64.hpp) ------
-// Every 32 x 32 block (query tile qt, key tile kt) of the dense M, in the lane
-// order of the attention's S^T accumulator: 64 lanes x 16 floats, lane
-// (h, q) holding M[32 kt + acc_row(r, h)][32 qt + q] at r = 0 .. 15 (acc_row:
-// pdsc_common.hpp), blocks qt-major: a wave reads its (qt, kt) block as 4
-// contiguous 16-B loads per lane.  Rows or columns past N hold 0.
-__host__ __device__ inline size_t mfrag_floats(int N) {
-    const size_t nt = mpack_ntile(N);
-    return nt * nt * MPACK_T * MPACK_T;
-}
-__host__ __device__ inline size_t mfrag_off(int qt, int kt, int nt) { return ((size_t)qt * nt + kt) * (MPACK_T * MPACK_T); }
 inline size_t align_bytes(size_t x) { return (x + 255) & ~size_t(255); }
 
 // fp16 planes per packed 1x1-conv weight (3xfp16 mode): 2 = hi + mid (22
@@ -171,10 +160,6 @@ hipError_t launch_compat(const float *src, const float *tgt, int B, int N, const
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,
                                 float *Mp, hipStream_t s, Ragged rg = {});
 
-// Mf: [B][mfrag_floats(N)] (the fragment-ordered layout of attention_w64)
-hipError_t launch_compat_frag(const float *src, const float *tgt, int B, int N, const float *sigma_d, float *Mf,
-                              hipStream_t s, Ragged rg = {});
-
 hipError_t launch_pack_dense(const float *w, const float *b, const float *bn_w, const float *bn_b,
                              const float *bn_rm, const float *bn_rv, int in, int out, bool f32, float *dst_w,
                              float *dst_b, float *dst_a, float *dst_beta, float *dst_scale, hipStream_t s);
@@ -183,20 +168,19 @@ hipError_t launch_copy(const float *src, float *dst, int n, hipStream_t s);
 // Attention partials for one layer: opart [B][nsplit][Npad x CH], ml [B][nsplit][Npad][2];
 // opart rows [Npad][CH] for f32, the fragment-block tiling of attention_h3.hpp
 // (h3_opart_off) for H3.
-// the split path's attention as attention_w64 (fragment-ordered M) for this shape?
+// the split path's attention as attention_w64 (64-query waves) for this shape?
 bool attention_w64(int B, int N, bool f32);
 int attention_nsplit(int B, int N, bool f32, bool w64 = false);
-// M's layouts: dense [B][N][N], symmetric-packed (mpack_*), fragment-ordered (mfrag_*)
-enum MLayout { M_DENSE = 0, M_PACKED = 1, M_FRAG = 2 };
+// M's layouts: dense [B][N][N], symmetric-packed (mpack_*)
+enum MLayout { M_DENSE = 0, M_PACKED = 1 };
 // q, k, v: the fp16 hi/lo split layouts of attention_h3.hpp (4 B per element),
 // or fp32 [B][Npad][CH] rows when f32 (exact-fp32 MFMA, attention.hpp).
-// M: dense [B][N][N], symmetric-packed [B][mpack_floats(N)] (H3) or fragment-ordered
-// [B][mfrag_floats(N)] (H3, attention_w64), per m_layout.
+// M: dense [B][N][N] or symmetric-packed [B][mpack_floats(N)] (H3), per m_layout.
 // vexp: [B][Npad/32] V-tile exponents of the H3 layout (attention_h3.hpp); unused for f32.
-// m_layout M_FRAG: attention_w64 (H3 only, nsplit from attention_nsplit(.., w64 = true)).
+// w64: attention_w64 (H3 and packed M only, nsplit from attention_nsplit(.., w64 = true)).
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
-                            int m_layout, bool f32, int B, int N, int Npad, int nsplit, float *opart, float *ml,
-                            hipStream_t s, Ragged rg = {});
+                            int m_layout, bool w64, bool f32, int B, int N, int Npad, int nsplit, float *opart,
+                            float *ml, hipStream_t s, Ragged rg = {});
 // attention_l fused with pw_mid_l (encoder.hip: attn_pw2_kernel) for this shape?
 bool attention_fused(int B, int N, bool f32);
 // attention of layer `layer` on (q, k, v, vexp_in) + the pointwise chain to the

@@ -52,24 +52,6 @@ def compat(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch
     return M
 
 
-def compat_frag(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch.Tensor:
-    """The fragment-ordered M of the 64-query-wave attention (include/pdsc.h:
-    pdsc_compat_frag_f32), re-laid out to dense [B,N,N] on the device for inspection."""
-    src, tgt = _dev(src, "src"), _dev(tgt, "tgt")
-    sigma_d = _dev(sigma_d.reshape(-1), "sigma_d")
-    B, N, _ = src.shape
-    L = _lib.load()
-    nf = L.pdsc_compat_frag_floats(N)
-    Mf = torch.empty((B, nf), dtype=torch.float32, device=src.device)
-    check(L.pdsc_compat_frag_f32(_p(src), _p(tgt), B, N, _p(sigma_d), _p(Mf), _stream(src.device)),
-          "pdsc_compat_frag_f32")
-    nt = (N + 31) // 32
-    # [B][qt][kt][lane (h, q)][r] -> M[32 kt + (r%4) + 8 (r//4) + 4 h][32 qt + q]
-    F = Mf.view(B, nt, nt, 2, 32, 4, 4)  # b, qt, kt, h, q, r//4 (g), r%4 (e)
-    full = F.permute(0, 2, 5, 3, 6, 1, 4).reshape(B, nt * 32, nt * 32)  # b, (kt, g, h, e), (qt, q)
-    return full[:, :N, :N].contiguous()
-
-
 def compat_packed(src: torch.Tensor, tgt: torch.Tensor, sigma_d: torch.Tensor) -> torch.Tensor:
     """The forward's symmetric-packed M (include/pdsc.h: pdsc_compat_packed_f32),
     unpacked to dense [B,N,N] on the device for inspection."""

@@ -74,9 +74,8 @@ def test_compat(name, gpu_device):
     M = kernels.compat(src, tgt, sd)[0]
     if "M" in g:
         assert np.array_equal(M.cpu().numpy(), g["M"])  # bit-exact
-    # the forward's two layouts hold the same bits (packed; fragment-ordered)
+    # the forward's packed layout holds the same bits
     assert torch.equal(kernels.compat_packed(src, tgt, sd)[0], M)
-    assert torch.equal(kernels.compat_frag(src, tgt, sd)[0], M)
     assert np.array_equal(torch.diagonal(M).cpu().numpy(), g["M_diag"])
     assert torch.equal(M, M.T)
     np.testing.assert_allclose(M.double().sum(-1).cpu().numpy(), g["M_row_sums"], rtol=1e-12, atol=1e-9)
@@ -661,12 +660,10 @@ def test_compat_bit_exact_random_scales(scale, sigma, gpu_device):
     sd = torch.tensor([sigma], dtype=torch.float32, device=gpu_device)
     M = kernels.compat(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
     Mp = kernels.compat_packed(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
-    Mf = kernels.compat_frag(_t(src, gpu_device), _t(tgt, gpu_device), sd).cpu().numpy()
     for b in range(B):
         ref = O.compat(src[b], tgt[b], float(np.float32(sigma)))
         assert np.array_equal(M[b], ref), b
         assert np.array_equal(Mp[b], ref), b
-        assert np.array_equal(Mf[b], ref), b
 
 
 @pytest.mark.parametrize("radius", [0.05, 0.1, 0.6])

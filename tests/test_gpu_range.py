@@ -132,7 +132,7 @@ def _plan2_child(path, sk):  # child process entry: the split-grid (PDSC_W64_SK=
 
 
 def test_range_guard_on_the_split_plan(gpu_device, tmp_path):
-    """The key-split plan (pdsc_encoder_plan 2: attention_w64 on fragment-ordered
+    """The key-split plan (pdsc_encoder_plan 2: attention_w64 on the packed
     M, stream-K by default and the split grid with PDSC_W64_SK=0), whose combine
     skips a split whose running max stayed -inf (fmaxf ignores NaN): a scaled
     pair among 8 x 5000 is still marked, its pose NaN and labels 0, every other

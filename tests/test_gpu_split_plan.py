@@ -1,8 +1,8 @@
 """The forward's split-path plan at the N = 5000 bench shape (run with -m gpu).
 
 8 pairs of 5000 correspondences: pdsc_encoder_plan reports 2 -- key-split
-attention on 64-query waves (attention_w64.hpp) over the fragment-ordered M
-(compat_frag_kernel) -- a plan no single-pair golden test reaches.  The batch
+attention on 64-query waves (attention_w64.hpp) over the symmetric-packed M
+(both load shapes of its M tiles) -- a plan no single-pair golden test reaches.  The batch
 mixes the N = 5000 goldens that share one network and the 3DMatch parameters
 (rel_5k, rel_5k_lo; a second batch holds rel_5k_kitti, whose sigma_d /
 thresholds differ),

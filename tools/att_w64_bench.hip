@@ -43,22 +43,6 @@ __global__ void fill_f(float *p, size_t n, unsigned seed) {
     p[i] = (x & 0xffff) / 65536.0f;
 }
 
-// packed M (attention_h3's layout) -> fragment-ordered M (attention_w64's)
-__global__ void packed_to_mfrag(const float *__restrict__ Mp, int N, float *__restrict__ Mf) {
-    const int nt = mpack_ntile(N), qt = blockIdx.x, kt = blockIdx.y, b = blockIdx.z, lane = threadIdx.x;
-    const float *P = Mp + (size_t)b * mpack_floats(N);
-    float *F = Mf + (size_t)b * mfrag_floats(N) + mfrag_off(qt, kt, nt) + 16 * lane;
-    for (int r = 0; r < 16; ++r) {
-        const int k = 32 * kt + acc_row(r, lane >> 5), q = 32 * qt + (lane & 31);
-        float v;
-        if (kt <= qt)
-            v = P[(size_t)mpack_tile(kt, qt, nt) * 1024 + (k & 31) * 32 + (q & 31)];
-        else
-            v = P[(size_t)mpack_tile(qt, kt, nt) * 1024 + (q & 31) * 32 + (k & 31)];
-        F[r] = v;
-    }
-}
-
 int main(int argc, char **argv) {
     const int B = argc > 1 ? atoi(argv[1]) : 128, N = argc > 2 ? atoi(argv[2]) : 1000;
     const int reps = argc > 3 ? atoi(argv[3]) : 20;
@@ -72,12 +56,11 @@ int main(int argc, char **argv) {
     const size_t rows = (size_t)B * gh.Npad * CH * 2, mper = mpack_floats(N);
     const int nsm = gh.nsplit > gw.nsplit ? gh.nsplit : gw.nsplit;
     _Float16 *Q, *K, *V;
-    float *M, *Mf, *vexp, *op, *ml, *op2, *ml2;
+    float *M, *vexp, *op, *ml, *op2, *ml2;
     CK(hipMalloc(&Q, rows * 2));
     CK(hipMalloc(&K, rows * 2));
     CK(hipMalloc(&V, rows * 2));
     CK(hipMalloc(&M, (size_t)B * mper * 4));
-    CK(hipMalloc(&Mf, (size_t)B * mfrag_floats(N) * 4));
     CK(hipMalloc(&vexp, (size_t)B * (gh.Npad / 32) * 4));
     CK(hipMalloc(&op, (size_t)B * nsm * gh.Npad * CH * 4));
     CK(hipMalloc(&ml, (size_t)B * nsm * gh.Npad * 2 * 4));
@@ -90,10 +73,6 @@ int main(int argc, char **argv) {
     if (getenv("BENCH_MONES")) {  // M = 1 (the M layouts out of the comparison)
         std::vector<float> ones((size_t)B * mper, 1.0f);
         CK(hipMemcpy(M, ones.data(), ones.size() * 4, hipMemcpyHostToDevice));
-    }
-    {
-        const int nt = mpack_ntile(N);
-        hipLaunchKernelGGL(packed_to_mfrag, dim3(nt, nt, B), dim3(64), 0, 0, M, N, Mf);
     }
     CK(hipMemset(vexp, 0, (size_t)B * (gh.Npad / 32) * 4));
     hipEvent_t a, b;
@@ -111,7 +90,7 @@ int main(int argc, char **argv) {
     };
     auto lw = [&] {
         hipLaunchKernelGGL((attention_w64_kernel<true>), dim3(gw.B * gw.nqb * gw.nsplit), dim3(256), W64_LDS + W64_ST_LDS, 0, Q, K,
-                           V, vexp, Mf, gw, op2, ml2);
+                           V, vexp, M, gw, op2, ml2);
     };
     auto timeit = [&](auto f) {
         for (int i = 0; i < 3; ++i) f();

@@ -52,25 +52,6 @@ __global__ __launch_bounds__(256) void store_rows(int N, float *M) {
         *reinterpret_cast<f32x4 *>(M + (size_t)i * N + j) = f32x4{1, 2, 3, 4};
 }
 
-// store-only, the fragment-ordered layout's pattern (compat_frag_kernel: per 64 x 64
-// block, each of its 32 x 32 tiles as one or two 4 KiB fragment blocks)
-__global__ __launch_bounds__(256) void store_frag(int N, int ntile, float *M) {
-    int t = blockIdx.x, ti = 0;
-    while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
-    const int tj = ti + t, nt32 = mpack_ntile(N);
-    M += (size_t)blockIdx.y * mfrag_floats(N);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int k = 0; k < 2; ++k) {
-        const int role = wave + 4 * k;
-        const int sr = (role >> 1) & 1, sc = role & 1, tpos = role >> 2;
-        const int tr = 2 * ti + sr, tcc = 2 * tj + sc;
-        if (tr > tcc || tr >= nt32 || tcc >= nt32 || (tpos && tr == tcc)) continue;
-        const int qt = tpos ? tr : tcc, kt = tpos ? tcc : tr;
-        float *blk = M + mfrag_off(qt, kt, nt32);
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4 *>(blk + 256 * g + 4 * lane) = f32x4{1, 2, 3, 4};
-    }
-}
-
 int main(int argc, char **argv) {
     int B = argc > 1 ? atoi(argv[1]) : 8, N = argc > 2 ? atoi(argv[2]) : 5000, iters = 10;
     const bool dm = argc > 3 && argv[3][0] == '3';  // 3DMatch-like: 30 % inliers under a rigid motion
@@ -89,7 +70,7 @@ int main(int argc, char **argv) {
         }
     }
     float *dp, *dM, *dsd;
-    CK(hipMalloc(&dp, hp.size() * 4)); CK(hipMalloc(&dM, (size_t)B * mfrag_floats(N) * 4)); CK(hipMalloc(&dsd, 4));
+    CK(hipMalloc(&dp, hp.size() * 4)); CK(hipMalloc(&dM, (size_t)B * N * N * 4)); CK(hipMalloc(&dsd, 4));
     float sd = 0.1f;
     CK(hipMemcpy(dp, hp.data(), hp.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dsd, &sd, 4, hipMemcpyHostToDevice));
@@ -100,12 +81,9 @@ int main(int argc, char **argv) {
         if (v == 2) hipLaunchKernelGGL(store_rows, dim3((N + 3) / 4, B), dim3(256), 0, 0, N, dM);
         if (v == 3) CK(launch_compat_packed(dp, dp + (size_t)B * N * 3, B, N, dsd, dM, 0));
         if (v == 4) hipLaunchKernelGGL(store_packed, dim3(ntri, B), dim3(256), 0, 0, N, ntile, dM);
-        if (v == 5) CK(launch_compat_frag(dp, dp + (size_t)B * N * 3, B, N, dsd, dM, 0));
-        if (v == 6) hipLaunchKernelGGL(store_frag, dim3(ntri, B), dim3(256), 0, 0, N, ntile, dM);
     };
-    const char *names[] = {"compat_kernel", "store-only tiles", "store-only rows", "compat_packed", "store-only packed",
-                           "compat_frag", "store-only frag"};
-    const int NV = 7;
+    const char *names[] = {"compat_kernel", "store-only tiles", "store-only rows", "compat_packed", "store-only packed"};
+    const int NV = 5;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     std::vector<std::vector<float>> t(NV);
