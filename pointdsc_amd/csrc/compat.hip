@@ -249,6 +249,14 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
         for (int q = 0; q < 4; ++q) {
             xs[q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
             xt[q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
+            // past N (padding of a ragged pair or of the last tile): stored as 0
+            // below; distances that pass compat4's zero test keep such elements
+            // out of its exact-evaluation queue (their points read as 0 would all
+            // queue: xs = xt = 0)
+            if (i0 + r >= N || j0 + cq * 4 + q >= N) {
+                xs[q] = 4.0f * s2;
+                xt[q] = 0.0f;
+            }
         }
         compat4(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
 #pragma unroll

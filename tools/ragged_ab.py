@@ -5,7 +5,7 @@
   ragged    bench.py's ragged leg: 128 pairs, N_b ~ U[700, 1300] (seeded as there),
   ragged1k  the same sizes scaled to mean 1000 exactly is not possible, so the
             ragged batch's correspondences / forward time is printed as corr/s.
-Usage: python tools/ragged_ab.py [reps]"""
+Usage: python tools/ragged_ab.py [reps]   (RAGGED_LEGS=uniform,padded,ragged: the legs to run)"""
 import os
 import sys
 import time
@@ -40,7 +40,11 @@ def main():
             out[b, :min(n_rows[b], len(q[key]))] = q[key][:n_rows[b]]
         return torch.from_numpy(out).to(dev)
 
-    def timeit(fn):
+    legs = os.environ.get("RAGGED_LEGS", "uniform,padded,ragged").split(",")
+
+    def timeit(fn, leg):
+        if leg not in legs:
+            return float("nan")
         for _ in range(2):
             fn()
         torch.cuda.synchronize(dev)
@@ -52,13 +56,13 @@ def main():
 
     pu = [synthetic_pair(1000, 7000 + i) for i in range(P)]
     cu, su, tu = (torch.from_numpy(np.stack([q[k] for q in pu])).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
-    t_uni = timeit(lambda: kernels.forward_testing(cfg, pk, cu, su, tu, check_range=False))
+    t_uni = timeit(lambda: kernels.forward_testing(cfg, pk, cu, su, tu, check_range=False), "uniform")
     cp, sp_, tp = (torch.zeros((P, Nmax, x.shape[2]), device=dev) for x in (cu, su, tu))
     cp[:, :1000], sp_[:, :1000], tp[:, :1000] = cu, su, tu
-    t_pad = timeit(lambda: kernels.forward_ragged(cfg, pk, cp, sp_, tp, [1000] * P, check_range=False))
+    t_pad = timeit(lambda: kernels.forward_ragged(cfg, pk, cp, sp_, tp, [1000] * P, check_range=False), "padded")
     rows = sizes
     cr, sr, tr = pad("corr_pos", rows), pad("src_keypts", rows), pad("tgt_keypts", rows)
-    t_rag = timeit(lambda: kernels.forward_ragged(cfg, pk, cr, sr, tr, sizes, check_range=False))
+    t_rag = timeit(lambda: kernels.forward_ragged(cfg, pk, cr, sr, tr, sizes, check_range=False), "ragged")
     print(f"{os.environ.get('AB_TAG', '')} uniform {t_uni:.3f} ms ({P * 1000 / t_uni * 1e3:.3g} corr/s) | "
           f"padded-to-{Nmax} {t_pad:.3f} ms | ragged {t_rag:.3f} ms ({sum(sizes) / t_rag * 1e3:.3g} corr/s, "
           f"sum n^2 / (128 x 1e6) = {sum(n * n for n in sizes) / (P * 1e6):.3f})", flush=True)
