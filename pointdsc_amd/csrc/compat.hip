@@ -20,14 +20,20 @@ namespace pdsc {
 
 constexpr int CT = 64;  // tile edge (dense kernel)
 
-// Per-wave LDS scratch of compat4: a queue of the elements that need the exact
-// evaluation and the wave's 4 x 64 outputs.
-struct CompatScratch {
-    float qx[256], qt[256], out[256];
-    unsigned short qs[256];
+// Rows of 4 columns per lane that compat_n evaluates in one call (the packed
+// kernel's 4 rows in 4 / COMPAT_RP calls).  Build knob for A/B: -DCOMPAT_RP=1|2|4.
+#ifndef COMPAT_RP
+#define COMPAT_RP 1
+#endif
+// Per-wave LDS scratch of compat_n<E> (E elements per lane): a queue of the
+// elements that need the exact evaluation and the wave's E x 64 outputs
+// (group-major: out[g][4 lane + e], so each lane's 16-B read is conflict-free).
+template <int E> struct CompatScratch {
+    float qx[64 * E], qt[64 * E], out[64 * E];
+    unsigned short qs[64 * E];
 };
 
-// M for 4 (row, column) pairs of this lane, given their squared distances.
+// M for E (row, column) pairs of this lane, given their squared distances.
 // M is 0 whenever |sqrt(xs) - sqrt(xt)| >= sigma_d, and
 //   |sqrt(xs) - sqrt(xt)| = |xs - xt| / (sqrt(xs) + sqrt(xt)) >= |xs - xt| / sqrt(2 (xs + xt)),
 // so (xs - xt)^2 > 2 s2 (xs + xt) (1 + 2^-10) proves M = 0 without a square
@@ -37,13 +43,16 @@ struct CompatScratch {
 // -- typically a fifth to a third -- are compacted into an LDS queue (ballot
 // order) and evaluated exactly, 64 per pass, so the ~40-op correctly rounded
 // sqrtf/sqrtf/'/' chain runs on full waves of useful work.
-PDSC_DEV void compat4(const float xs[4], const float xt[4], float s2, float rs2, bool s2ok, float kzero,
-                      float gmax, CompatScratch &sc, int lane, float out[4]) {
+template <int E>
+PDSC_DEV void compat_n(const float (&xs)[E], const float (&xt)[E], float s2, float rs2, bool s2ok, float kzero,
+                       float gmax, CompatScratch<E> &sc, int lane, float (&out)[E]) {
     const unsigned long long below = (1ull << lane) - 1ull;
-    *reinterpret_cast<f32x4 *>(&sc.out[4 * lane]) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int g = 0; g < E / 4; ++g)
+        *reinterpret_cast<f32x4 *>(&sc.out[256 * g + 4 * lane]) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     int cnt = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < E; ++q) {
         const float dxt = xs[q] - xt[q], sum = xs[q] + xt[q];
         const bool zero = (dxt * dxt > kzero * sum) && (sum <= gmax);  // NaN, xs = xt = 0 -> exact path
         const unsigned long long m = __ballot(!zero);
@@ -51,7 +60,7 @@ PDSC_DEV void compat4(const float xs[4], const float xt[4], float s2, float rs2,
             const int pos = cnt + __popcll(m & below);
             sc.qx[pos] = xs[q];
             sc.qt[pos] = xt[q];
-            sc.qs[pos] = (unsigned short)(4 * lane + q);
+            sc.qs[pos] = (unsigned short)(256 * (q >> 2) + 4 * lane + (q & 3));
         }
         cnt += __popcll(m);
     }
@@ -72,9 +81,12 @@ PDSC_DEV void compat4(const float xs[4], const float xt[4], float s2, float rs2,
         if (act) sc.out[sc.qs[e]] = m > 0.0f ? m : 0.0f;
     }
     __builtin_amdgcn_wave_barrier();
-    const f32x4 o = *reinterpret_cast<const f32x4 *>(&sc.out[4 * lane]);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[q] = o[q];
+    for (int g = 0; g < E / 4; ++g) {
+        const f32x4 o = *reinterpret_cast<const f32x4 *>(&sc.out[256 * g + 4 * lane]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[4 * g + q] = o[q];
+    }
     __builtin_amdgcn_wave_barrier();  // the next call rewrites sc
 }
 
@@ -194,7 +206,8 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
                                                             const float *__restrict__ sigma_d_ptr,
                                                             float *__restrict__ Mp, Ragged rg) {
     __shared__ float pts[4][CT][3];  // row src, row tgt, col src, col tgt
-    __shared__ CompatScratch scr[4];
+    constexpr int RP = COMPAT_RP, E = 4 * RP;  // rows per compat_n call, elements per lane
+    __shared__ CompatScratch<E> scr[4];
     int t = blockIdx.x, ti = 0;
     while (t >= ntile - ti) { t -= ntile - ti; ++ti; }
     const int tj = ti + t;
@@ -209,7 +222,7 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
     const float s2 = sd * sd;
     const float rs2 = 1.0f / s2;
     const bool s2ok = s2 >= 1.17549435e-38f && s2 < 1e30f && rs2 >= 1.17549435e-38f;
-    const float kzero = 2.0f * s2 * (1.0f + 0x1p-10f), gmax = 0x1p20f * s2;  // compat4's zero test
+    const float kzero = 2.0f * s2 * (1.0f + 0x1p-10f), gmax = 0x1p20f * s2;  // compat_n's zero test
     src += (size_t)b * Nstr * 3;
     tgt += (size_t)b * Nstr * 3;
     const int nt32 = mpack_ntile(Nstr);
@@ -235,36 +248,41 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
             ct[q][k] = pts[3][cq * 4 + q][k];
         }
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int r = rq + 16 * rr;
-        const int tr = 2 * ti + (r >> 5);
-        // below the diagonal (diagonal block) / past N: computed (compat4 needs the
-        // whole wave) but not stored
-        const bool skip = tr > tc || tr >= nt32 || tc >= nt32;
-        if (__all(skip)) continue;  // wave-uniform
-        const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
-        const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
-        float xs[4], xt[4], out[4];
+    for (int r0 = 0; r0 < 4; r0 += RP) {
+        // rows rq + 16 rr, rr = r0 .. r0 + RP - 1.  Elements below the diagonal
+        // (diagonal blocks) or past N are not stored: their distances are set to
+        // pass compat_n's zero test, so they never queue for the exact path.
+        bool skip[RP], any = false;
+        float xs[E], xt[E], out[E];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            xs[q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
-            xt[q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
-            // past N (padding of a ragged pair or of the last tile): stored as 0
-            // below; distances that pass compat4's zero test keep such elements
-            // out of its exact-evaluation queue (their points read as 0 would all
-            // queue: xs = xt = 0)
-            if (i0 + r >= N || j0 + cq * 4 + q >= N) {
-                xs[q] = 4.0f * s2;
-                xt[q] = 0.0f;
+        for (int u = 0; u < RP; ++u) {
+            const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
+            skip[u] = tr > tc || tr >= nt32 || tc >= nt32;
+            any |= !skip[u];
+            const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
+            const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xs[4 * u + q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
+                xt[4 * u + q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
+                if (skip[u] || i0 + r >= N || j0 + cq * 4 + q >= N) {
+                    xs[4 * u + q] = 4.0f * s2;
+                    xt[4 * u + q] = 0.0f;
+                }
             }
         }
-        compat4(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
+        if (!__any(any)) continue;  // wave-uniform
+        compat_n<E>(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (i0 + r >= N || j0 + cq * 4 + q >= N) out[q] = 0.0f;
-        if (skip) continue;
-        float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
-        *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{out[0], out[1], out[2], out[3]};
+        for (int u = 0; u < RP; ++u) {
+            if (skip[u]) continue;
+            const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
+            float o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (i0 + r >= N || j0 + cq * 4 + q >= N) ? 0.0f : out[4 * u + q];
+            float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
+            *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{o[0], o[1], o[2], o[3]};
+        }
     }
 }
 

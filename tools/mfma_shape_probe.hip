@@ -3,7 +3,8 @@
 // it for bf16): every CU runs 4 waves (one per SIMD, or 8 = two per SIMD), each
 // a long loop of v_mfma_f32_32x32x16_f16 or v_mfma_f32_16x16x32_f16 on random
 // fp16 operands re-read from LDS every step (as the attention reads K/V
-// fragments), 4 independent accumulators.  Equal FLOP per variant; prints the
+// fragments; 32x32x16: 2 x 2 fragments -> 4 MFMAs, 16x16x32: 4 x 4 -> 16, the
+// same LDS bytes per FLOP), independent accumulators.  Prints the
 // wall TFLOP/s of back-to-back launches (~2 s each) and the in-kernel clock
 // (s_memtime / s_memrealtime x 100 MHz).
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/mfma_shape_probe.hip -o tools/mfma_shape_probe
@@ -17,7 +18,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
-// SHAPE 0: 32x32x16 (32768 MACs per instruction), 1: 16x16x32 (8192: four per 32x32x16)
+// SHAPE 0: 32x32x16 (16384 MACs per instruction), 1: 16x16x32 (8192)
 template <int SHAPE>
 __global__ __launch_bounds__(512) void probe(const f16x8 *in, float *out, unsigned long long *clk, int iters) {
     __shared__ __attribute__((aligned(16))) f16x8 lds[1024];  // 16 KiB of random fp16
@@ -43,15 +44,17 @@ __global__ __launch_bounds__(512) void probe(const f16x8 *in, float *out, unsign
         f32x4 c[16] = {};
         for (int it = 0; it < iters; ++it) {
             const int base = ((it * 8 + wave) & 15) * 64;
-            const f16x8 a0 = lds[base + lane], b0 = lds[(base + 64 * 3 + lane) & 1023];
-            const f16x8 a1 = lds[(base + 64 * 5 + lane) & 1023], b1 = lds[(base + 64 * 7 + lane) & 1023];
+            f16x8 a[4], b[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                c[4 * j + 0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, c[4 * j + 0], 0, 0, 0);
-                c[4 * j + 1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0, c[4 * j + 1], 0, 0, 0);
-                c[4 * j + 2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, c[4 * j + 2], 0, 0, 0);
-                c[4 * j + 3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b1, c[4 * j + 3], 0, 0, 0);
+                a[j] = lds[(base + 64 * (2 * j) + lane) & 1023];
+                b[j] = lds[(base + 64 * (2 * j + 1) + lane) & 1023];
             }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    c[4 * i + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], c[4 * i + j], 0, 0, 0);
         }
         float s = 0.0f;
         for (int j = 0; j < 16; ++j) s += c[j][0] + c[j][1] + c[j][2] + c[j][3];
@@ -107,7 +110,8 @@ int main() {
             std::vector<double> ghz;
             for (int i = 0; i < WG; ++i) ghz.push_back((double)hc[2 * i] / (double)hc[2 * i + 1] * 0.1);
             std::sort(ghz.begin(), ghz.end());
-            const double flop = 2.0 * 32768.0 * 4.0 * iters * waves * WG * n;  // per launch x launches
+            // MACs per iteration and wave: 4 x 32x32x16 = 65536, 16 x 16x16x32 = 131072
+            const double flop = 2.0 * (shape == 0 ? 65536.0 : 131072.0) * iters * waves * WG * n;
             printf("waves/CU %d shape %s: %.1f TFLOP/s (fp16 dense), in-kernel clock median %.2f GHz, %d launches\n",
                    waves, shape == 0 ? "32x32x16" : "16x16x32", flop / el * 1e-12, ghz[WG / 2], n);
             fflush(stdout);
