@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, v_mfma_f32_32x32x2_f32
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense v_mfma_f32_32x32x16_f16
+MEASURED_F16_MFMA_TFLOPS = 1287.8  # profiles/r05_mfma_shape.log: 32x32x16 f16, all CUs, random operands
 # the attention computes each fp32 product as 3 fp16 MFMA products (hi.hi + hi.lo + lo.hi,
 # attention_h3.hpp): its ceiling in ALGORITHMIC (fp32) flop/s is the fp16 peak / 3
 PEAK_H3_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
@@ -396,6 +397,12 @@ def main():
                     "peak_note": "fp16 MFMA 2500 TFLOP/s / 3 products per fp32 product (the attention's and, "
                                  "from r04, the fused chain's convolutions'); exact-fp32 MFMA peak is 157.3",
                     "fp16_mfma_util": round(3 * achieved / PEAK_F16_MFMA_TFLOPS, 4),
+                    # context, not the roofline: the fp16 MFMA rate the chip sustains on random
+                    # operands with every CU busy (the clock falls under load), measured by
+                    # tools/mfma_shape_probe.hip (profiles/r05_mfma_shape.log), per 3 products
+                    "measured_ceiling": {"value": round(MEASURED_F16_MFMA_TFLOPS / 3, 1), "unit": "TFLOP/s",
+                                         "frac": round(achieved / (MEASURED_F16_MFMA_TFLOPS / 3), 4),
+                                         "source": "tools/mfma_shape_probe.hip, two waves per SIMD, 1.71 GHz"},
                     "launch_ms": round(att_ms, 4), "launches_timed": len(att_times),
                     "flop_per_launch": flops, "share_of_step": round(n_launch * att_ms / ms_per_step, 3)}
         sp = ctypes.c_void_p(stream.cuda_stream)
