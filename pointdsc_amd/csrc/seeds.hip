@@ -158,6 +158,9 @@ PDSC_DEV uint32_t float_key(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// float_key's inverse (-0 comes back as +0, which compares equal to it; NaN bits kept)
+PDSC_DEV float key_float(uint32_t k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k); }
+
 PDSC_DEV int pow2_at_least(int n) {
     int P = 64;
     while (P < n) P <<= 1;
@@ -178,6 +181,119 @@ __global__ __launch_bounds__(SORT_NT) void seed_rank_sort_kernel(const float *__
                          : ~0ull;
     bitonic_sort_u64(skeys, P, tid);
     for (int r = tid; r < S; r += SORT_NT) seeds[(size_t)b * Sstr + r] = (int)(unsigned)skeys[r];
+}
+
+// ------------------------------------------------------------------ select form
+// The seed ranking of seed_rank_kernel in O(N + C^2) per pair: one 256-thread
+// workgroup per pair radix-selects tau = the key of the S-th largest score
+// (order-preserving keys of conf * lm, -0 keyed as +0, 8-bit digits in LDS
+// histograms), collects the C >= S candidates with key >= tau and ranks them
+// among themselves -- every j that outranks a candidate (a larger score, or an
+// equal one at a lower index) is itself a candidate, so
+//   rank_i = #{j in C : k_j > k_i} + #{j in C : k_j == k_i, j < i}
+// is exactly seed_rank_kernel's count, bit for bit.  Candidates beyond
+// SEL_CMAX (a tie at tau spanning many points) or a NaN score (whose compare
+// ranks differ from any order): every row is ranked against all N instead, the
+// compare kernel's loop.
+constexpr int SEL_NT = 256, SEL_CMAX = 2048;
+
+__global__ __launch_bounds__(SEL_NT) void seed_select_kernel(const float *__restrict__ conf,
+                                                             const float *__restrict__ lm, int Nstr, int Sstr,
+                                                             int *__restrict__ seeds, Ragged rg) {
+    extern __shared__ uint32_t selk[];  // [N] keys, then [SEL_CMAX] candidate indices
+    __shared__ int hist[256];
+    __shared__ int sh_digit, sh_need, sh_cnt, sh_nan;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    int *cand = reinterpret_cast<int *>(selk + Nstr);
+    conf += (size_t)b * Nstr;
+    lm += (size_t)b * Nstr;
+    seeds += (size_t)b * Sstr;
+    if (tid == 0) {
+        sh_nan = 0;
+        sh_cnt = 0;
+    }
+    __syncthreads();
+    int nan = 0;
+    for (int i = tid; i < N; i += SEL_NT) {
+        const float sc = conf[i] * lm[i];  // (:217)
+        nan |= sc != sc;
+        selk[i] = float_key(sc);
+    }
+    if (nan) atomicOr(&sh_nan, 1);
+    // radix select of the S-th largest key, most significant digit first
+    uint32_t prefix = 0, mask = 0;
+    int need = S;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < N; i += SEL_NT) {
+            const uint32_t k = selk[i];
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1);
+        }
+        __syncthreads();
+        if (tid < 64) {  // wave 0: the digit holding the need-th largest, scanning down
+            int acc = 0, d = -1;
+            for (int g = 3; g >= 0 && d < 0; --g) {
+                const int bin = 64 * g + tid, c = hist[bin];
+                // suffix sums from bin 64 g + 63 down to this lane's bin
+                int suf = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_down(suf, o);
+                    if (tid + o < 64) suf += v;
+                }
+                const bool hit = acc + suf >= need && acc + suf - c < need;
+                const unsigned long long m = __ballot(hit);
+                if (m) {
+                    const int l = __ffsll((long long)m) - 1;
+                    const int above = __shfl(acc + suf - c, l);
+                    d = 64 * g + l;
+                    if (tid == 0) {
+                        sh_digit = d;
+                        sh_need = need - above;
+                    }
+                }
+                acc += __shfl(suf, 0);
+            }
+        }
+        __syncthreads();
+        prefix |= (uint32_t)sh_digit << shift;
+        mask |= 255u << shift;
+        need = sh_need;
+        __syncthreads();
+    }
+    // candidates: key >= tau (= prefix)
+    for (int i = tid; i < N; i += SEL_NT)
+        if (selk[i] >= prefix) {
+            const int p = atomicAdd(&sh_cnt, 1);
+            if (p < SEL_CMAX) cand[p] = i;
+        }
+    __syncthreads();
+    const int C = sh_cnt;
+    if (sh_nan || C > SEL_CMAX) {  // workgroup-uniform: the compare ranking of every row
+        for (int i = tid; i < N; i += SEL_NT) {
+            const float si = key_float(selk[i]);
+            int rank = 0;
+            for (int j = 0; j < N; ++j) {
+                const float sj = key_float(selk[j]);
+                rank += (sj > si) || (sj == si && j < i);
+            }
+            if (rank < S) seeds[rank] = i;
+        }
+        return;
+    }
+    for (int q = tid; q < C; q += SEL_NT) {
+        const int i = cand[q];
+        const uint32_t ki = selk[i];
+        int rank = 0;
+        for (int r = 0; r < C; ++r) {
+            const int j = cand[r];
+            const uint32_t kj = selk[j];
+            rank += (kj > ki) || (kj == ki && j < i);
+        }
+        if (rank < S) seeds[rank] = i;
+    }
 }
 
 __global__ __launch_bounds__(SORT_NT) void local_max_sort_kernel(const float *__restrict__ src,
@@ -280,9 +396,27 @@ hipError_t launch_local_max(const float *src, const float *conf, int B, int N, f
     return hipGetLastError();
 }
 
+// The select form (seed_select_kernel) from 64 pairs (one workgroup each) where
+// its keys and candidates fit the workgroup's LDS.  Measured (A/B, one box):
+// 128 x 1000 forward 3.768 vs 3.778 ms; with a workgroup per pair it loses to the
+// compare kernels' many workgroups at 8 x 5000 (4.392 vs 4.376) and one pair
+// (0.429 vs 0.422).  A/B knob PDSC_SEED_SELECT (measurement only): 0 never, 1
+// at every batch size.
+static bool seed_select_on(int B, int N) {
+    static const int mode = [] {
+        const char *e = getenv("PDSC_SEED_SELECT");
+        return e ? atoi(e) : 2;
+    }();
+    if (mode == 0 || (size_t)N * 4 + SEL_CMAX * 4 > 64 * 1024) return false;
+    return mode == 1 || B >= 64;
+}
+
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
                             hipStream_t s, Ragged rg) {
-    if (seed_sort_on() && N <= SORT_MAX)
+    if (seed_select_on(B, N) && !seed_sort_on())
+        hipLaunchKernelGGL(seed_select_kernel, dim3(B), dim3(SEL_NT), (size_t)N * 4 + SEL_CMAX * 4, s, conf, lm, N, S,
+                           seeds, rg);
+    else if (seed_sort_on() && N <= SORT_MAX)
         hipLaunchKernelGGL(seed_rank_sort_kernel, dim3(B), dim3(SORT_NT), sort_lds(N), s, conf, lm, N, S, seeds, rg);
     else if (seed_small(B, N))
         hipLaunchKernelGGL(seed_rank_kernel<16>, dim3((N + 15) / 16, B), dim3(256), 0, s, conf, lm, N, S, seeds, rg);

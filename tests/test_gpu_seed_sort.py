@@ -1,7 +1,10 @@
-"""The opt-in sorted forms of a5 (seeds.hip: bitonic-sorted NMS window and seed
-ranking, knob PDSC_SEED_SORT=1, measurement only) give exactly the compare
-kernels' bits: is_local_max and the seed list, on tie-heavy scores, -0 / +0
-scores, negative local maxima and duplicate points (run with -m gpu)."""
+"""The other forms of a5 give exactly the compare kernels' bits: the opt-in
+sorted forms (seeds.hip: bitonic-sorted NMS window and seed ranking, knob
+PDSC_SEED_SORT=1, measurement only) and the default select form of the ranking
+(radix-selected threshold + candidate ranking, seed_select_kernel; knob
+PDSC_SEED_SELECT=0 for the compare kernel): is_local_max and the seed list, on
+tie-heavy scores, -0 / +0 scores, negative local maxima and duplicate points,
+and ties at the threshold wider than the candidate buffer (run with -m gpu)."""
 import os
 import subprocess
 import sys
@@ -13,7 +16,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 CASES = [(3, 1000, 100, 0.1), (2, 5000, 500, 0.1), (1, 777, 77, 0.6), (4, 64, 6, 0.05), (1, 6000, 600, 1e-3),
-         (2, 3000, 300, 0.02)]
+         (2, 3000, 300, 0.02), (1, 9000, 4000, 0.02), (2, 2000, 1999, 0.0)]
 
 
 def _inputs(B, N, seed):
@@ -41,11 +44,13 @@ def _dump(path):
 def test_seed_kernel_forms_bit_identical(gpu_device, tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for tag, env in (("full", dict(PDSC_SEED_SORT="0")), ("sort", dict(PDSC_SEED_SORT="1"))):
+    for tag, env in (("full", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="0")), ("sort", dict(PDSC_SEED_SORT="1")),
+                     ("select", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="1"))):
         path = tmp_path / f"seeds_{tag}.npz"
         code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
                f"import test_gpu_seed_sort as t; t._dump({str(path)!r})"
         subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), check=True, timeout=240)
         res[tag] = np.load(path)
-    for k in res["full"].files:
-        assert np.array_equal(res["full"][k], res["sort"][k]), k
+    for form in ("sort", "select"):
+        for k in res["full"].files:
+            assert np.array_equal(res["full"][k], res[form][k]), (form, k)
