@@ -205,6 +205,7 @@ __global__ __launch_bounds__(SEL_NT) void seed_select_kernel(const float *__rest
     __shared__ int sh_digit, sh_need, sh_cnt, sh_nan;
     const int b = blockIdx.x, tid = threadIdx.x;
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    if (S < 1 || N < 1) return;  // workgroup-uniform: no seed to place
     int *cand = reinterpret_cast<int *>(selk + Nstr);
     conf += (size_t)b * Nstr;
     lm += (size_t)b * Nstr;
