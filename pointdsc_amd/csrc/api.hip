@@ -197,7 +197,7 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
         const bool timed = g_tcap > 0 && g_tcount && *g_tcount < g_tcap;
         if (timed) HIPCHK(hipEventRecord(g_tstart[*g_tcount], s));
         HIPCHK(launch_attention(e.q, e.k, e.v, e.vexp, M, m_layout, w64, d.f32, d.B, d.N, d.Npad, d.nsplit, e.opart,
-                                e.ml, s, rg));
+                                e.ml, s, rg, l));
         if (timed) HIPCHK(hipEventRecord(g_tstop[(*g_tcount)++], s));
         const float *op = e.opart, *mlp = e.ml;
         int ns = d.nsplit;

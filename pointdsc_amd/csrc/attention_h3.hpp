@@ -265,6 +265,7 @@ struct AttnGridH3 {
     // ragged batches: pair b's correspondences (N, Npad: the batch's strides), or null
     const int *nv;
     const int *po;  // ragged batches: workgroup pair slot -> pair (Ragged::po), or null
+    int rev = 0;    // the workgroup order reversed (alternate layers: attn_pw2 ZIGZAG)
     PDSC_DEV int n(int b) const { return nv ? nv[b] : N; }
 };
 
@@ -319,8 +320,14 @@ PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
     const int G = g.B * g.nqb * g.nsplit;
     int lid = blockIdx.x;
     if (xcd) {
+        // g.rev: each XCD walks its own logical range backwards (pairs keep their XCD)
         const int full = G & ~7;
-        if (lid < full) lid = (lid & 7) * (full >> 3) + (lid >> 3);
+        if (lid < full) {
+            const int loc = lid >> 3;
+            lid = (lid & 7) * (full >> 3) + (g.rev ? (full >> 3) - 1 - loc : loc);
+        }
+    } else if (g.rev) {
+        lid = G - 1 - lid;
     }
     const int slot = lid / g.nsplit / g.nqb;
     return AttnBlock{g.po ? g.po[slot] : slot, (lid / g.nsplit) % g.nqb, lid % g.nsplit};

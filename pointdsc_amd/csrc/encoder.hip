@@ -142,6 +142,20 @@ static int att_target() {
     return t;
 }
 static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, N, att_target()); }
+
+// The attention's workgroup order, reversed on alternate layers (fused and
+// split-K launches; the stream-K form excepted): a launch
+// starts on the pairs whose M (and featL) the previous one read last, while
+// they may still sit in the Infinity Cache.  A/B knob PDSC_ZIGZAG=0 (measurement
+// only).
+static int zigzag_rev(int layer) {
+    static const int mode = [] {
+        const char *e = getenv("PDSC_ZIGZAG");
+        return e ? atoi(e) : 1;
+    }();
+    return mode == 0 ? 0 : mode == 2 ? !(layer & 1) : (layer & 1);
+}
+
 // PDSC_PRECISION_F32: attention.hpp's exact-fp32 MFMA kernel, 32-key stages, libm expf
 constexpr int ATT_F32_KTS = 32;
 static AttnGrid f32_grid(int B, int N) { return attention_grid<ATT_NW, ATT_F32_KTS>(B, N, att_target()); }
@@ -189,7 +203,7 @@ int attention_nsplit(int B, int N, bool f32, bool w64) {
 
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             int m_layout, bool w64, bool f32, int B, int N, int Npad, int nsplit, float *opart,
-                            float *ml, hipStream_t s, Ragged rg) {
+                            float *ml, hipStream_t s, Ragged rg, int layer) {
     const bool m_packed = m_layout == M_PACKED;
     if (w64) {  // attention_w64 (H3 layouts, symmetric-packed M)
         if (f32 || !m_packed) return hipErrorInvalidValue;
@@ -205,6 +219,7 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
         }
         g.nv = rg.nv;
         g.po = rg.po;
+        g.rev = rg.po ? 0 : zigzag_rev(layer);
         hipLaunchKernelGGL((attention_w64_kernel<true>), dim3(g.B * g.nqb * g.nsplit), dim3(W64_NW * 64), W64_LDS, s,
                            static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
                            static_cast<const _Float16 *>(v), vexp, M, g, opart, ml);
@@ -226,6 +241,7 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     AttnGridH3 g = prod_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
+    g.rev = rg.po ? 0 : zigzag_rev(layer);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     const dim3 grid(g.B * g.nqb * g.nsplit), block(ATT_NW * 64);
     const size_t lds = attention_h3_lds_bytes<ATT_NW>();
@@ -1764,6 +1780,7 @@ hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
+    g.rev = rg.po ? 0 : zigzag_rev(layer);  // (ragged batches keep their longest-first order)
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad || layer + 1 >= lay.L) return hipErrorInvalidValue;
     const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));
     const size_t lds = std::max(attention_h3_lds_bytes<PW2_W>(), PW2_LDS);
@@ -1786,6 +1803,7 @@ hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, cons
     AttnGridH3 g = fused_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
+    g.rev = rg.po ? 0 : zigzag_rev(lay.L - 1);
     if (g.nsplit != 1 || g.Npad != Npad || g.nqb * PW2_PTS != Npad) return hipErrorInvalidValue;
     W2Sched S = sched_msg(msg3(lay.layer[lay.L - 1]));
     w2_sched_add(S, lay.c0, CH, CLS);

@@ -180,7 +180,7 @@ enum MLayout { M_DENSE = 0, M_PACKED = 1 };
 // w64: attention_w64 (H3 and packed M only, nsplit from attention_nsplit(.., w64 = true)).
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             int m_layout, bool w64, bool f32, int B, int N, int Npad, int nsplit, float *opart,
-                            float *ml, hipStream_t s, Ragged rg = {});
+                            float *ml, hipStream_t s, Ragged rg = {}, int layer = 0);
 // attention_l fused with pw_mid_l (encoder.hip: attn_pw2_kernel) for this shape?
 bool attention_fused(int B, int N, bool f32);
 // attention of layer `layer` on (q, k, v, vexp_in) + the pointwise chain to the
