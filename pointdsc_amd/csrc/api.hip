@@ -731,7 +731,8 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s, rg));
-    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s, rg));
+    // (kdist, written by the seed kNN next, is the ranking's scratch)
+    HIPCHK(launch_seed_rank(f.conf, f.lm, d.B, d.N, d.S, f.seeds, s, rg, reinterpret_cast<uint32_t *>(f.kdist)));
     STAGE(3);
     // a6 (:250-252)
     RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.knn, s, rg));

@@ -224,8 +224,9 @@ hipError_t launch_pw_last(const float *packed, const PackLayout &lay, bool f32, 
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s, Ragged rg = {});
+// scratch: B S N words the ranking may use (the forward's kdist), or null
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
-                            hipStream_t s, Ragged rg = {});
+                            hipStream_t s, Ragged rg = {}, uint32_t *scratch = nullptr);
 
 // ns: normed as [B][N][2][128] fp16 hi/lo (qk_pos order, attention_h3.hpp)
 hipError_t launch_knn_dist(const _Float16 *ns, const int *seeds, int B, int N, int S, float *dist,

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict_
 #pragma unroll 8
         for (int jj = sl * PER; jj < sl * PER + jn; ++jj) {
             const float sj = ss[jj];
-            rank += (sj > si) || (sj == si && j0 + jj < i);
+            rank += (int)((sj > si) | ((sj == si) & (j0 + jj < i)));  // bitwise: no branch per compare
         }
     }
     part[sl][il] = rank;
@@ -184,29 +184,45 @@ __global__ __launch_bounds__(SORT_NT) void seed_rank_sort_kernel(const float *__
 }
 
 // ------------------------------------------------------------------ select form
-// The seed ranking of seed_rank_kernel in O(N + C^2) per pair: one 256-thread
-// workgroup per pair radix-selects tau = the key of the S-th largest score
-// (order-preserving keys of conf * lm, -0 keyed as +0, 8-bit digits in LDS
-// histograms), collects the C >= S candidates with key >= tau and ranks them
-// among themselves -- every j that outranks a candidate (a larger score, or an
-// equal one at a lower index) is itself a candidate, so
-//   rank_i = #{j in C : k_j > k_i} + #{j in C : k_j == k_i, j < i}
-// is exactly seed_rank_kernel's count, bit for bit.  Candidates beyond
-// SEL_CMAX (a tie at tau spanning many points) or a NaN score (whose compare
-// ranks differ from any order): every row is ranked against all N instead, the
-// compare kernel's loop.
-constexpr int SEL_NT = 256, SEL_CMAX = 2048;
+// The seed ranking of seed_rank_kernel in O(N + A^2) per pair, one 1024-thread
+// workgroup per pair:
+//  1. radix-select tau = the key of the S-th largest score (order-preserving
+//     keys of conf * lm, -0 keyed as +0, 8-bit digits in LDS histograms whose
+//     atomics are aggregated per wave for the wave's most common digit: most
+//     scores are the zero of a point that is no local maximum);
+//  2. the A < S candidates with key > tau are ranked among themselves -- every
+//     j that outranks one (a larger score, or an equal one at a lower index) is
+//     itself a candidate -- their keys and indices packed contiguously (one 8-B
+//     broadcast read per compare), each candidate's count split over NT / A
+//     threads that meet in an LDS sum;
+//  3. places A .. S-1 are the first S - A points with key == tau in index order
+//     (an ordered compaction: per-thread index ranges + a workgroup scan).
+// rank_i = #{j : k_j > k_i} + #{j < i : k_j == k_i}, exactly seed_rank_kernel's
+// count, bit for bit.  A > SEL_CMAX or a NaN score (whose compare ranks differ
+// from any order): every row is ranked against all N instead, the compare
+// kernel's loop.
+constexpr int SEL_NT = 1024, SEL_CMAX = 2048;
 
+__host__ __device__ constexpr size_t sel_lds(int N) { return (size_t)((N + 1) & ~1) * 4 + (size_t)SEL_CMAX * 12; }
+
+// SPLIT: step 2 is left to seed_cand_rank_kernel (many workgroups per pair): the
+// candidates go to `scratch` (per pair at b Sstr Nstr words: keys [Sstr], indices
+// [Sstr], A) instead.
+template <bool SPLIT>
 __global__ __launch_bounds__(SEL_NT) void seed_select_kernel(const float *__restrict__ conf,
                                                              const float *__restrict__ lm, int Nstr, int Sstr,
-                                                             int *__restrict__ seeds, Ragged rg) {
-    extern __shared__ uint32_t selk[];  // [N] keys, then [SEL_CMAX] candidate indices
+                                                             int *__restrict__ seeds, uint32_t *__restrict__ scratch,
+                                                             Ragged rg) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t selk[];  // [N] keys | [SEL_CMAX] (key, index) | [SEL_CMAX] ranks
     __shared__ int hist[256];
+    __shared__ int wtot[SEL_NT / 64];
     __shared__ int sh_digit, sh_need, sh_cnt, sh_nan;
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
-    if (S < 1 || N < 1) return;  // workgroup-uniform: no seed to place
-    int *cand = reinterpret_cast<int *>(selk + Nstr);
+    if (S < 1 || N < 1) return;  // workgroup-uniform: no seed to place (seed_cand_rank_kernel leaves too)
+    if (SPLIT) scratch += (size_t)b * Sstr * Nstr;
+    uint2 *cand = reinterpret_cast<uint2 *>(selk + ((Nstr + 1) & ~1));
+    int *crank = reinterpret_cast<int *>(cand + SEL_CMAX);
     conf += (size_t)b * Nstr;
     lm += (size_t)b * Nstr;
     seeds += (size_t)b * Sstr;
@@ -224,13 +240,22 @@ __global__ __launch_bounds__(SEL_NT) void seed_select_kernel(const float *__rest
     if (nan) atomicOr(&sh_nan, 1);
     // radix select of the S-th largest key, most significant digit first
     uint32_t prefix = 0, mask = 0;
-    int need = S;
+    int need = min(S, N);
     for (int shift = 24; shift >= 0; shift -= 8) {
-        hist[tid] = 0;
+        if (tid < 256) hist[tid] = 0;
         __syncthreads();
         for (int i = tid; i < N; i += SEL_NT) {
             const uint32_t k = selk[i];
-            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1);
+            const bool in = (k & mask) == prefix;
+            const int d = (int)((k >> shift) & 255u);
+            const unsigned long long act = __ballot(in);
+            if (act) {
+                const int lead = __ffsll((long long)act) - 1;
+                const int d0 = __shfl(d, lead);
+                const unsigned long long same = __ballot(in && d == d0);
+                if (lane == lead) atomicAdd(&hist[d0], __popcll(same));
+                else if (in && d != d0) atomicAdd(&hist[d], 1);
+            }
         }
         __syncthreads();
         if (tid < 64) {  // wave 0: the digit holding the need-th largest, scanning down
@@ -262,39 +287,110 @@ __global__ __launch_bounds__(SEL_NT) void seed_select_kernel(const float *__rest
         prefix |= (uint32_t)sh_digit << shift;
         mask |= 255u << shift;
         need = sh_need;
-        __syncthreads();
     }
-    // candidates: key >= tau (= prefix)
+    // tau = prefix; need = how many of the points with key == tau are seeds
+    // candidates: key > tau, in any order
     for (int i = tid; i < N; i += SEL_NT)
-        if (selk[i] >= prefix) {
+        if (selk[i] > prefix) {
             const int p = atomicAdd(&sh_cnt, 1);
-            if (p < SEL_CMAX) cand[p] = i;
+            if (p < SEL_CMAX) {
+                cand[p] = uint2{selk[i], (uint32_t)i};
+                crank[p] = 0;
+            }
         }
     __syncthreads();
-    const int C = sh_cnt;
-    if (sh_nan || C > SEL_CMAX) {  // workgroup-uniform: the compare ranking of every row
+    const int A = sh_cnt;
+    if (sh_nan || A > SEL_CMAX) {  // workgroup-uniform: the compare ranking of every row
+        if (SPLIT && tid == 0) scratch[2 * Sstr] = 0;  // nothing for seed_cand_rank_kernel
         for (int i = tid; i < N; i += SEL_NT) {
             const float si = key_float(selk[i]);
             int rank = 0;
             for (int j = 0; j < N; ++j) {
                 const float sj = key_float(selk[j]);
-                rank += (sj > si) || (sj == si && j < i);
+                rank += (int)((sj > si) | ((sj == si) & (j < i)));
             }
             if (rank < S) seeds[rank] = i;
         }
         return;
     }
-    for (int q = tid; q < C; q += SEL_NT) {
-        const int i = cand[q];
-        const uint32_t ki = selk[i];
-        int rank = 0;
-        for (int r = 0; r < C; ++r) {
-            const int j = cand[r];
-            const uint32_t kj = selk[j];
-            rank += (kj > ki) || (kj == ki && j < i);
+    // places A .. A + need - 1: the first `need` points with key == tau, by index
+    {
+        const int chunk = (N + SEL_NT - 1) / SEL_NT, i0 = tid * chunk, i1 = min(N, i0 + chunk);
+        int c = 0;
+        for (int i = i0; i < i1; ++i) c += selk[i] == prefix;
+        int inc = c;  // inclusive scan over the wave, then over the waves
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o);
+            if (lane >= o) inc += v;
         }
-        if (rank < S) seeds[rank] = i;
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        int pos = A + inc - c;
+        for (int w = 0; w < wave; ++w) pos += wtot[w];
+        for (int i = i0; i < i1 && pos < A + need; ++i)
+            if (selk[i] == prefix) seeds[pos++] = i;
     }
+    if (SPLIT) {
+        for (int q = tid; q < A; q += SEL_NT) {
+            scratch[q] = cand[q].x;
+            scratch[Sstr + q] = cand[q].y;
+        }
+        if (tid == 0) scratch[2 * Sstr] = (uint32_t)A;
+        return;
+    }
+    // places 0 .. A - 1: candidate q's count over the r-slice `part` of P slices
+    const int P = A > 0 ? max(1, SEL_NT / A) : 1, len = A > 0 ? (A + P - 1) / P : 0;
+    for (int t = tid; t < A * P; t += SEL_NT) {
+        const int q = t % A, part = t / A;
+        const uint2 ci = cand[q];
+        int rank = 0;
+        const int r1 = min(A, (part + 1) * len);
+#pragma unroll 4
+        for (int r = part * len; r < r1; ++r) {
+            const uint2 cj = cand[r];
+            rank += (int)((cj.x > ci.x) | ((cj.x == ci.x) & (cj.y < ci.y)));
+        }
+        if (P == 1) crank[q] = rank;
+        else if (rank) atomicAdd(&crank[q], rank);
+    }
+    __syncthreads();
+    for (int q = tid; q < A; q += SEL_NT) seeds[crank[q]] = (int)cand[q].y;
+}
+
+// Step 2 of the split select: workgroup (x, b) ranks pair b's candidates
+// 64 x .. 64 x + 63 against all A of them (four threads per candidate, each a
+// quarter of the A compares, summed in LDS) -- A^2 compares over A / 64
+// workgroups instead of one.
+constexpr int SEL_RQ = 64;
+
+__global__ __launch_bounds__(256) void seed_cand_rank_kernel(const uint32_t *__restrict__ scratch, int Nstr,
+                                                             int Sstr, int *__restrict__ seeds, Ragged rg) {
+    __shared__ uint2 c[SEL_CMAX];
+    __shared__ int part[4][SEL_RQ];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);
+    if (S < 1 || N < 1) return;  // workgroup-uniform (seed_select_kernel wrote nothing)
+    scratch += (size_t)b * Sstr * Nstr;
+    const int A = (int)scratch[2 * Sstr], q0 = blockIdx.x * SEL_RQ;
+    if (q0 >= A) return;  // workgroup-uniform
+    for (int r = tid; r < A; r += 256) c[r] = uint2{scratch[r], scratch[Sstr + r]};
+    __syncthreads();
+    const int q = q0 + (tid & (SEL_RQ - 1)), p = tid / SEL_RQ, len = (A + 3) / 4;
+    int rank = 0;
+    if (q < A) {
+        const uint2 ci = c[q];
+        const int r1 = min(A, (p + 1) * len);
+#pragma unroll 4
+        for (int r = p * len; r < r1; ++r) {
+            const uint2 cj = c[r];
+            rank += (int)((cj.x > ci.x) | ((cj.x == ci.x) & (cj.y < ci.y)));
+        }
+    }
+    part[p][tid & (SEL_RQ - 1)] = rank;
+    __syncthreads();
+    if (tid < SEL_RQ && q < A)
+        seeds[(size_t)b * Sstr + part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]] = (int)c[q].y;
 }
 
 __global__ __launch_bounds__(SORT_NT) void local_max_sort_kernel(const float *__restrict__ src,
@@ -397,27 +493,41 @@ hipError_t launch_local_max(const float *src, const float *conf, int B, int N, f
     return hipGetLastError();
 }
 
-// The select form (seed_select_kernel) from 64 pairs (one workgroup each) where
-// its keys and candidates fit the workgroup's LDS.  Measured (A/B, one box):
-// 128 x 1000 forward 3.768 vs 3.778 ms; with a workgroup per pair it loses to the
-// compare kernels' many workgroups at 8 x 5000 (4.392 vs 4.376) and one pair
-// (0.429 vs 0.422).  A/B knob PDSC_SEED_SELECT (measurement only): 0 never, 1
-// at every batch size.
+// The select form (seed_select_kernel) where the compare kernels' B N^2 work is
+// large (>= 1e8 compares: 128 x 1000, 8 x 5000) and its keys and candidates fit
+// the workgroup's LDS; split in two launches (seed_cand_rank_kernel: the A^2
+// candidate compares over many workgroups) from S > 256 when the caller has
+// scratch.  Measured (rocprofv3, one box): 128 x 1000 13.2 us vs 15.8 for the
+// first select form (256 threads, every compare through an index) and ~26 for
+// seed_rank_kernel<64>; one N = 1000 pair 9.5 vs 5.4 (seed_rank_kernel<16>).
+// A/B knob PDSC_SEED_SELECT (measurement only): 0 never, 1 at every batch size.
 static bool seed_select_on(int B, int N) {
     static const int mode = [] {
         const char *e = getenv("PDSC_SEED_SELECT");
         return e ? atoi(e) : 2;
     }();
-    if (mode == 0 || (size_t)N * 4 + SEL_CMAX * 4 > 64 * 1024) return false;
-    return mode == 1 || B >= 64;
+    if (mode == 0 || sel_lds(N) > 64 * 1024) return false;
+    return mode == 1 || (double)B * N * N >= 1e8;
 }
 
 hipError_t launch_seed_rank(const float *conf, const float *lm, int B, int N, int S, int *seeds,
-                            hipStream_t s, Ragged rg) {
-    if (seed_select_on(B, N) && !seed_sort_on())
-        hipLaunchKernelGGL(seed_select_kernel, dim3(B), dim3(SEL_NT), (size_t)N * 4 + SEL_CMAX * 4, s, conf, lm, N, S,
-                           seeds, rg);
-    else if (seed_sort_on() && N <= SORT_MAX)
+                            hipStream_t s, Ragged rg, uint32_t *scratch) {
+    if (seed_select_on(B, N) && !seed_sort_on()) {
+        // scratch per pair: 2 S + 1 <= S N words
+        static const bool split_off = [] {  // A/B knob PDSC_SEL_SPLIT=0 (measurement only)
+            const char *e = getenv("PDSC_SEL_SPLIT");
+            return e && e[0] == '0';
+        }();
+        if (scratch && S > 256 && N >= 3 && !split_off) {
+            hipLaunchKernelGGL(seed_select_kernel<true>, dim3(B), dim3(SEL_NT), sel_lds(N), s, conf, lm, N, S, seeds,
+                               scratch, rg);
+            hipLaunchKernelGGL(seed_cand_rank_kernel, dim3(SEL_CMAX / SEL_RQ, B), dim3(256), 0, s, scratch, N, S,
+                               seeds, rg);
+        } else {
+            hipLaunchKernelGGL(seed_select_kernel<false>, dim3(B), dim3(SEL_NT), sel_lds(N), s, conf, lm, N, S, seeds,
+                               nullptr, rg);
+        }
+    } else if (seed_sort_on() && N <= SORT_MAX)
         hipLaunchKernelGGL(seed_rank_sort_kernel, dim3(B), dim3(SORT_NT), sort_lds(N), s, conf, lm, N, S, seeds, rg);
     else if (seed_small(B, N))
         hipLaunchKernelGGL(seed_rank_kernel<16>, dim3((N + 15) / 16, B), dim3(256), 0, s, conf, lm, N, S, seeds, rg);
