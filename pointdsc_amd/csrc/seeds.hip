@@ -77,6 +77,94 @@ __global__ __launch_bounds__(256) void local_max_kernel(const float *__restrict_
     }
 }
 
+// The same NMS with RPT rows per thread (rows blockIdx.x SQ RPT + r SQ + il):
+// each LDS point feeds RPT compares (the one-row kernel above reads 16 B of LDS
+// per compare and measured LDS-bound: packing its arithmetic cut VALU 8 -> 5.25
+// per compare at unchanged time), and row pairs share packed fp32 arithmetic
+// (v_pk_add / v_pk_mul / v_pk_fma_f32 against the point splat, the same
+// per-component rounding as sqdist3).
+template <int SQ, int RPT>
+__global__ __launch_bounds__(256) void local_max_rows_kernel(const float *__restrict__ src,
+                                                             const float *__restrict__ conf, int Nstr, float R2,
+                                                             float *__restrict__ lm, Ragged rg) {
+    static_assert(RPT % 2 == 0, "row pairs");
+    constexpr int NSL = 256 / SQ, PER = SEED_TILE / NSL, NP = RPT / 2;
+    __shared__ f32x4 tile[SEED_TILE];
+    __shared__ unsigned char part[NSL][SQ * RPT];
+    const int b = blockIdx.y, tid = threadIdx.x, sl = tid / SQ, il = tid % SQ;
+    const int i0 = blockIdx.x * SQ * RPT + il;
+    const int N = rg.n(b, Nstr);  // this pair's points; Nstr: the row stride
+    if (blockIdx.x * SQ * RPT >= N) return;  // workgroup-uniform
+    src += (size_t)b * Nstr * 3;
+    conf += (size_t)b * Nstr;
+    f32x2 xi[NP], yi[NP], zi[NP];
+    float ci[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int i = i0 + r * SQ;
+        const bool in = i < N;
+        const float x = in ? src[3 * i] : 0.0f, y = in ? src[3 * i + 1] : 0.0f, z = in ? src[3 * i + 2] : 0.0f;
+        xi[r / 2][r & 1] = x;
+        yi[r / 2][r & 1] = y;
+        zi[r / 2][r & 1] = z;
+        ci[r] = in ? conf[i] : 0.0f;
+    }
+    bool ok[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) ok[r] = true;
+    for (int j0 = 0; j0 < N; j0 += SEED_TILE) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < SEED_TILE / 256; ++e) {
+            const int t = tid + 256 * e, j = j0 + t;
+            // padding points never violate: conf -inf
+            tile[t] = (j < N) ? f32x4{src[3 * j], src[3 * j + 1], src[3 * j + 2], conf[j]}
+                              : f32x4{0.0f, 0.0f, 0.0f, -INFINITY};
+        }
+        __syncthreads();
+        // violation: c_i < c_j and !(|s_i - s_j| >= R), the latter as !(x >= R2) on the
+        // squared norm (sqrt_ge_threshold: exact, no sqrtf, branch-free)
+        bool bad[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) bad[r] = false;
+        // the padded tail skipped per wave: lane 0's slice (the wave's lowest) has the
+        // most points; the higher slices' extra points are other slices' points or
+        // padding (conf -inf), both harmless to an OR of violations, and a
+        // wave-uniform trip count keeps the loop scalar and unrolled
+        const int jn = __builtin_amdgcn_readfirstlane(min(PER, max(N - j0 - sl * PER, 0)));
+        const f32x4 *ts = tile + sl * PER;
+#pragma unroll 4
+        for (int t = 0; t < jn; ++t) {
+            const f32x4 pj = ts[t];
+            const f32x2 xj = {pj[0], pj[0]}, yj = {pj[1], pj[1]}, zj = {pj[2], pj[2]};
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const f32x2 dx = xi[q] - xj, dy = yi[q] - yj, dz = zi[q] - zj;
+                const f32x2 x = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+                bad[2 * q] |= (ci[2 * q] < pj[3]) & !(x[0] >= R2);
+                bad[2 * q + 1] |= (ci[2 * q + 1] < pj[3]) & !(x[1] >= R2);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RPT; ++r)
+            if (bad[r]) ok[r] = false;
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) part[sl][r * SQ + il] = ok[r];
+    __syncthreads();
+    if (sl == 0) {
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const int i = i0 + r * SQ;
+            if (i >= N) continue;
+            int all = 1;
+#pragma unroll
+            for (int q = 0; q < NSL; ++q) all &= part[q][r * SQ + il];
+            lm[(size_t)b * Nstr + i] = all ? 1.0f : 0.0f;
+        }
+    }
+}
+
 template <int SQ>
 __global__ __launch_bounds__(256) void seed_rank_kernel(const float *__restrict__ conf,
                                                         const float *__restrict__ lm, int Nstr, int Sstr,
@@ -478,12 +566,36 @@ static bool seed_sort_on() {
 }
 static size_t sort_lds(int N) { return (size_t)std::max(64, 1 << (32 - __builtin_clz((unsigned)std::max(N - 1, 1)))) * 8; }
 
+// rows per thread of the NMS compare kernel: 1 (local_max_kernel); A/B knob
+// PDSC_LM_RPT=2|4 (local_max_rows_kernel, measurement only)
+static int lm_rpt() {
+    static const int r = [] {
+        const char *e = getenv("PDSC_LM_RPT");
+        return e ? atoi(e) : 1;
+    }();
+    return r;
+}
+
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
                             float *lm, hipStream_t s, Ragged rg) {
     if (seed_sort_on() && N <= NMS_SORT_MAX) {
         const size_t lds = sort_lds(N) + (size_t)N * sizeof(f32x4);
         hipLaunchKernelGGL(local_max_sort_kernel, dim3((N + SORT_NT - 1) / SORT_NT, B), dim3(SORT_NT), lds, s, src, conf,
                            N, sqrt_ge_threshold(radius), lm, rg);
+    } else if (lm_rpt() == 4) {
+        if (seed_small(B, N))
+            hipLaunchKernelGGL((local_max_rows_kernel<16, 4>), dim3((N + 63) / 64, B), dim3(256), 0, s, src, conf, N,
+                               sqrt_ge_threshold(radius), lm, rg);
+        else
+            hipLaunchKernelGGL((local_max_rows_kernel<64, 4>), dim3((N + 255) / 256, B), dim3(256), 0, s, src, conf,
+                               N, sqrt_ge_threshold(radius), lm, rg);
+    } else if (lm_rpt() == 2) {
+        if (seed_small(B, N))
+            hipLaunchKernelGGL((local_max_rows_kernel<16, 2>), dim3((N + 31) / 32, B), dim3(256), 0, s, src, conf, N,
+                               sqrt_ge_threshold(radius), lm, rg);
+        else
+            hipLaunchKernelGGL((local_max_rows_kernel<64, 2>), dim3((N + 127) / 128, B), dim3(256), 0, s, src, conf,
+                               N, sqrt_ge_threshold(radius), lm, rg);
     } else if (seed_small(B, N))
         hipLaunchKernelGGL(local_max_kernel<16>, dim3((N + 15) / 16, B), dim3(256), 0, s, src, conf, N,
                            sqrt_ge_threshold(radius), lm, rg);
