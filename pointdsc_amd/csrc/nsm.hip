@@ -210,7 +210,7 @@ constexpr int KNN_FASTCAP = 128;
 
 template <int R>
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int Nstr, int Sstr,
-                                                         int k, int *__restrict__ knn, Ragged rg) {
+                                                         int k, int *__restrict__ knn, Ragged rg, int bitonic) {
     __shared__ uint32_t hist[4][256];
     __shared__ uint32_t ckey[4][64];
     __shared__ int cidx[4][64];
@@ -306,6 +306,31 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 }
                 c += __popcll(m);
             }
+        }
+        if (bitonic && c <= 64) {  // wave-uniform
+            // the c <= 64 candidates sorted by (key, index) across the wave (a
+            // 21-stage bitonic network of lane-pair exchanges): lane r then holds
+            // rank r, the same order the compare ranking below computes
+            __builtin_amdgcn_wave_barrier();
+            uint32_t kk = lane < (int)c ? fkeyb[wave][lane] : 0xffffffffu;
+            int ii = lane < (int)c ? fidxb[wave][lane] : 0x7fffffff;
+#pragma unroll
+            for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+                for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                    const uint32_t ok = (uint32_t)__shfl_xor((int)kk, stride);
+                    const int oi = __shfl_xor(ii, stride);
+                    const bool other_less = (ok < kk) | ((ok == kk) & (oi < ii));
+                    // the lower lane of an ascending pair (or the upper of a descending one) keeps the smaller
+                    const bool keep_small = ((lane & stride) == 0) == ((lane & size) == 0);
+                    if (keep_small == other_less) {
+                        kk = ok;
+                        ii = oi;
+                    }
+                }
+            int *out = knn + ((size_t)b * Sstr + s) * k;
+            if (lane > 0 && lane < (int)want && lane < (int)c) out[lane - 1] = ii;  // drop position 0 (:68)
+            return;
         }
         if (c <= KNN_FASTCAP) {
             __builtin_amdgcn_wave_barrier();
@@ -487,22 +512,26 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const int R = (N + 63) / 64;
+    static const int bit = [] {  // A/B knob PDSC_KNN_BITONIC=1: the sorted rank of <= 64 candidates
+        const char *e = getenv("PDSC_KNN_BITONIC");
+        return e ? atoi(e) : 0;
+    }();
     if (R <= 16)
-        hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 32)
-        hipLaunchKernelGGL(knn_select_kernel<32>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<32>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 48)
-        hipLaunchKernelGGL(knn_select_kernel<48>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<48>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 64)
-        hipLaunchKernelGGL(knn_select_kernel<64>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<64>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 80)
-        hipLaunchKernelGGL(knn_select_kernel<80>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<80>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 96)
-        hipLaunchKernelGGL(knn_select_kernel<96>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<96>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else if (R <= 128)
-        hipLaunchKernelGGL(knn_select_kernel<128>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<128>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     else
-        hipLaunchKernelGGL(knn_select_kernel<0>, grid, block, 0, s, dist, N, S, k, knn, rg);
+        hipLaunchKernelGGL(knn_select_kernel<0>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
     return hipGetLastError();
 }
 
