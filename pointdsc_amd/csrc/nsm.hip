@@ -512,9 +512,12 @@ hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int 
     const int wpb = seed_wpb(B, S);
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const int R = (N + 63) / 64;
-    static const int bit = [] {  // A/B knob PDSC_KNN_BITONIC=1: the sorted rank of <= 64 candidates
+    // the fast path's <= 64 candidates ranked by a wave bitonic sort (128 x 1000:
+    // 36.5 vs 40.1 us per launch; 8 x 5000 and one pair equal); A/B knob
+    // PDSC_KNN_BITONIC=0: the readlane compare ranking (measurement only)
+    static const int bit = [] {
         const char *e = getenv("PDSC_KNN_BITONIC");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     if (R <= 16)
         hipLaunchKernelGGL(knn_select_kernel<16>, grid, block, 0, s, dist, N, S, k, knn, rg, bit);
