@@ -1142,6 +1142,10 @@ PDSC_DEV void block_sum(float (&v)[NV], float (*red)[NV], int tid) {
     __syncthreads();
 }
 
+template <typename WF>
+PDSC_DEV void block_rigid_h(const float *__restrict__ A, const float *__restrict__ Bp, int n, WF wfun,
+                            const float (&s7)[7], float *Tout, float (*red)[9], int tid);
+
 // rigid_transform_3d on (A, B, w) rows [0, n) (models/common.py:7-45).
 // wfun(i) returns the weight of row i (0 drops it).
 template <typename WF>
@@ -1159,6 +1163,14 @@ PDSC_DEV void block_rigid(const float *__restrict__ A, const float *__restrict__
         s7[6] += Bp[3 * i + 2] * w;
     }
     block_sum<7>(s7, reinterpret_cast<float (*)[7]>(red), tid);
+    block_rigid_h(A, Bp, n, wfun, s7, Tout, red, tid);
+}
+
+// block_rigid's second half: the centroids from the block-summed weight and
+// weighted coordinate sums s7 = (sum w, sum w A, sum w B), then H and the solve.
+template <typename WF>
+PDSC_DEV void block_rigid_h(const float *__restrict__ A, const float *__restrict__ Bp, int n, WF wfun,
+                            const float (&s7)[7], float *Tout, float (*red)[9], int tid) {
     const float den = s7[0] + 1e-6f;
     const float cA[3] = {s7[1] / den, s7[2] / den, s7[3] / den};
     const float cB[3] = {s7[4] / den, s7[5] / den, s7[6] / den};
@@ -1196,16 +1208,6 @@ __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ tra
         float T[12];
 #pragma unroll
         for (int e = 0; e < 12; ++e) T[e] = Ts[e];
-        float c1[1] = {0.0f};
-        for (int n = tid; n < N; n += RB) {
-            const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
-                                      tb[3 * n + 2]);
-            c1[0] += (L2 < thr) ? 1.0f : 0.0f;
-        }
-        block_sum<1>(c1, reinterpret_cast<float (*)[1]>(red), tid);
-        const int cnt = (int)c1[0];
-        if (cnt == prev) break;  // abs(int(inlier_num - previous_inlier_num)) < 1 (:426)
-        prev = cnt;
         auto wfun = [&](int n) -> float {
             const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
                                       tb[3 * n + 2]);
@@ -1213,8 +1215,34 @@ __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ tra
             const float r = L2 / thr;
             return 1.0f / (1.0f + r * r);  // 1/(1 + (L2/thr)^2) (:435)
         };
+        // one pass: the inlier count (:423-426) and block_rigid's weighted sums of
+        // the same T (the next iterate's weights), in block_rigid's order
+        float c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int n = tid; n < N; n += RB) {
+            const float ax = sb[3 * n], ay = sb[3 * n + 1], az = sb[3 * n + 2];
+            const float bx = tb[3 * n], by = tb[3 * n + 1], bz = tb[3 * n + 2];
+            const float L2 = residual(T, ax, ay, az, bx, by, bz);
+            float w = 0.0f;
+            if (L2 < thr) {
+                const float r = L2 / thr;
+                w = 1.0f / (1.0f + r * r);
+                c8[7] += 1.0f;
+            }
+            c8[0] += w;
+            c8[1] += ax * w;
+            c8[2] += ay * w;
+            c8[3] += az * w;
+            c8[4] += bx * w;
+            c8[5] += by * w;
+            c8[6] += bz * w;
+        }
+        block_sum<8>(c8, reinterpret_cast<float (*)[8]>(red), tid);
+        const int cnt = (int)c8[7];
+        if (cnt == prev) break;  // abs(int(inlier_num - previous_inlier_num)) < 1 (:426)
+        prev = cnt;
+        const float s7[7] = {c8[0], c8[1], c8[2], c8[3], c8[4], c8[5], c8[6]};
         float Tn[16];
-        block_rigid(sb, tb, N, wfun, Tn, red, tid);
+        block_rigid_h(sb, tb, N, wfun, s7, Tn, red, tid);
         if (tid == 0)
             for (int e = 0; e < 16; ++e) Ts[e] = Tn[e];
         __syncthreads();
