@@ -596,6 +596,31 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
 // same wave runs the power iteration.  No workgroup barriers: waves are
 // independent.
 constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
+// T build on packed fp32 (source, target) pairs; 0: the scalar form (A/B builds)
+#ifndef NSM_PK_TBUILD
+#define NSM_PK_TBUILD 1
+#endif
+// cr_sqrt / cr_div (pdsc_common.hpp) on two lanes' worth of operands: the
+// fma corrections as v_pk_fma_f32, the same operations per component.
+PDSC_DEV f32x2 cr_sqrt2(f32x2 x) {
+    const f32x2 s = {__builtin_amdgcn_sqrtf(x[0]), __builtin_amdgcn_sqrtf(x[1])};
+    const f32x2 dn = {__uint_as_float(__float_as_uint(s[0]) - 1u), __uint_as_float(__float_as_uint(s[1]) - 1u)};
+    const f32x2 up = {__uint_as_float(__float_as_uint(s[0]) + 1u), __uint_as_float(__float_as_uint(s[1]) + 1u)};
+    const f32x2 rdn = __builtin_elementwise_fma(-dn, s, x), rup = __builtin_elementwise_fma(-up, s, x);
+    f32x2 r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        float v = rdn[i] <= 0.0f ? dn[i] : s[i];
+        v = rup[i] > 0.0f ? up[i] : v;
+        r[i] = x[i] == 0.0f ? x[i] : v;
+    }
+    return r;
+}
+PDSC_DEV f32x2 cr_div2(f32x2 x, f32x2 d, f32x2 rcp) {
+    const f32x2 q = x * rcp;
+    const f32x2 r = __builtin_elementwise_fma(-q, d, x);
+    return __builtin_elementwise_fma(r, rcp, q);
+}
 // LDS row stride of T for KC-padded rows: 16-B aligned, 13 (KC + 4) / 4 mod 16
 // distinct 16-B banks groups over 16 consecutive rows (conflict-free ds_read_b128)
 __host__ __device__ constexpr int nsm_tstride(int kc) { return kc + 4; }
@@ -666,8 +691,14 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
     const float p0 = ps[0], p1 = ps[1], p2 = ps[2], p3 = pt[0], p4 = pt[1], p5 = pt[2];
     auto store_p = [&] {
         if (lane < k) {
+#if NSM_PK_TBUILD
+            // (src, tgt) interleaved per axis: the T build's packed fp32 pairs
+            *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{p0, p3, p1, p4};
+            *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{p2, p5, 0.0f, 0.0f};
+#else
             *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR) = f32x4{p0, p1, p2, p3};
             *reinterpret_cast<f32x4 *>(P + lane * NSM_PSTR + 4) = f32x4{p4, p5, 0.0f, 0.0f};
+#endif
         }
         NSM_STAMP(2);
     };
@@ -779,6 +810,21 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         // (r04: the hardware square root and a reciprocal multiply in the H3 build,
         // -22 VALU per pair, flipped one borderline pair of the recall-parity
         // proxy -- test_recall_parity_synthetic -- so both modes keep these.)
+#if NSM_PK_TBUILD
+        // the source and target halves as packed fp32 pairs (v_pk_add / mul /
+        // fma_f32): per component the same operations in the same order as the
+        // scalar form below, so the same bits
+        const f32x2 dx = f32x2{pa0[0], pa0[1]} - f32x2{pc0[0], pc0[1]};
+        const f32x2 dy = f32x2{pa0[2], pa0[3]} - f32x2{pc0[2], pc0[3]};
+        const f32x2 dz = f32x2{pa1[0], pa1[1]} - f32x2{pc1[0], pc1[1]};
+        const f32x2 d2 = (dx * dx + dy * dy) + dz * dz;                       // :268 (src, tgt)
+        const f32x2 st = cr_sqrt2(d2);
+        const float dd = st[0] - st[1];
+        // (1 - g) / sigma^2 and dd^2 / sigma_d^2 as one packed correctly rounded division
+        const f32x2 qd = cr_div2(f32x2{1.0f - g, dd * dd}, f32x2{sig2, sd2}, f32x2{rsig2, rsd2});
+        const f32x2 om = f32x2{1.0f, 1.0f} - qd;
+        const float val = fmaxf(om[0], 0.0f) * fmaxf(om[1], 0.0f);            // :259, :270, :277
+#else
         const float fm = fmaxf(1.0f - cr_div(1.0f - g, sig2, rsig2), 0.0f);  // :259
         float dx = pa0[0] - pc0[0], dy = pa0[1] - pc0[1], dz = pa0[2] - pc0[2];
         const float ds = cr_sqrt((dx * dx + dy * dy) + dz * dz);    // :268
@@ -789,6 +835,7 @@ __global__ __launch_bounds__(256, 4) void nsm_seed_kernel(const void *__restrict
         const float dd = ds - dt;
         const float sm = fmaxf(1.0f - cr_div(dd * dd, sd2, rsd2), 0.0f);     // :270
         const float val = fm * sm;                                            // :277
+#endif
         Tl[a * tls + c] = val;
         Tl[c * tls + a] = val;
     }
