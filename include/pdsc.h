@@ -405,6 +405,10 @@ int32_t pdsc_forward_testing_debug(const pdsc_config *cfg, const float *packed, 
  * ratio) >= 1.  debug: as pdsc_forward_testing_debug (may be NULL), with the
  * batch's strides S = int(N * ratio) and k; conf rows past counts[b], and seeds,
  * knn and weights entries past a pair's own seeds, are unspecified.
+ * From 32 pairs on the fused encoder plan the encoder runs as two half batches,
+ * one on `stream` and one on a per-device side stream the library owns, forked
+ * from and joined back into `stream` by events (still asynchronous; the same
+ * results as one stream; environment PDSC_ENC_HALVES=0 keeps one stream).
  * Workspace: pdsc_forward_workspace_bytes(cfg, B, N).                        */
 int32_t pdsc_forward_testing_ragged(const pdsc_config *cfg, const float *packed, const float *corr_pos,
                                     const float *src, const float *tgt, int32_t B, int32_t N,

@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -216,6 +217,95 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
                                   d.f32 ? nullptr : normed_s, conf, s));
         }
     }
+    return PDSC_OK;
+}
+
+// Ragged batches run the fused encoder as two half batches of pairs on two
+// streams (the caller's and a per-device side stream, forked and joined by
+// events), so one half's launches fill the other's dispatch tails: a ragged
+// batch's attention launches end in a tail of a few long workgroups per XCD
+// (DESIGN.md §7).  Pairs are independent through the encoder, so each half is
+// the same arithmetic on its own pointer range (bitwise equal results).
+// 128 pairs, N in [700, 1300]: 4.54 -> 4.12 ms per forward; uniform batches
+// (two full rounds of workgroups, no tail to fill) measured 3.77 -> 3.83 ms, so
+// they stay on one stream.  Knob PDSC_ENC_HALVES: 0 never, 1 uniform batches too.
+static int enc_halves_mode() {
+    static const int v = [] {
+        const char *e = getenv("PDSC_ENC_HALVES");
+        return e && e[0] == '0' ? 0 : (e && e[0] == '1' ? 2 : 1);
+    }();
+    return v;
+}
+static bool enc_halves(const Dims &d, bool ragged) {
+    const int mode = enc_halves_mode();
+    return d.fuse && d.B >= 32 && (mode == 2 || (mode == 1 && ragged));
+}
+
+struct SideStream {
+    std::mutex mu;  // one fork / join enqueued at a time per device
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream *side_stream() {
+    static SideStream ss[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &x = ss[dev];
+    static std::mutex create_mu;
+    std::lock_guard<std::mutex> lock(create_mu);
+    if (!x.join) {  // all three or none (a failure leaves the forward on one stream)
+        if (!x.s2 && hipStreamCreateWithFlags(&x.s2, hipStreamNonBlocking) != hipSuccess) x.s2 = nullptr;
+        if (x.s2 && !x.fork && hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) x.fork = nullptr;
+        if (x.fork && hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) x.join = nullptr;
+    }
+    return x.join ? &x : nullptr;
+}
+
+// The fused plan's encoder over pairs [b0, b0 + nb): every per-pair pointer
+// moved to pair b0 (the pair-major layouts of carve_encoder / carve_forward).
+static int run_encoder_part(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
+                            int m_layout, const Dims &d, const EncBufs &e, float *normed, _Float16 *normed_s,
+                            float *conf, hipStream_t s, Ragged rg, int b0, int nb) {
+    Dims dh = d;
+    dh.B = nb;
+    const size_t rows = (size_t)b0 * d.Npad * CH;
+    EncBufs eh = e;
+    eh.feat = e.feat + rows;
+    eh.q = e.q + 2 * rows;
+    eh.k = e.k + 2 * rows;
+    eh.v = e.v + 2 * rows;
+    eh.q2 = e.q2 + 2 * rows;
+    eh.k2 = e.k2 + 2 * rows;
+    eh.v2 = e.v2 + 2 * rows;
+    eh.vexp = e.vexp + (size_t)b0 * (d.Npad / 32);
+    eh.vexp2 = e.vexp2 + (size_t)b0 * (d.Npad / 32);
+    const size_t mstr = m_layout == M_PACKED ? mpack_floats(d.N) : (size_t)d.N * d.N;
+    Ragged rh = rg;
+    if (rg.nv) rh.nv = rg.nv + b0;
+    if (rg.sv) rh.sv = rg.sv + b0;
+    if (rg.po) rh.po = rg.po + b0;
+    return run_encoder(lay, packed, corr_pos + (size_t)b0 * d.N * lay.in_dim, M + (size_t)b0 * mstr, m_layout, dh,
+                       eh, nullptr, normed + (size_t)b0 * d.N * CH, normed_s + (size_t)b0 * d.N * 2 * CH,
+                       conf + (size_t)b0 * d.N, s, rh);
+}
+
+// run_encoder for the forward: the fused plan as two concurrent halves given a
+// side stream ss (enc_halves; rg.po, when set, must then order each half's
+// pairs on its own: launch_ragged_order per half), else run_encoder itself.
+static int run_encoder_fwd(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
+                           int m_layout, const Dims &d, const EncBufs &e, float *normed, _Float16 *normed_s,
+                           float *conf, hipStream_t s, Ragged rg, SideStream *ss) {
+    if (!ss) return run_encoder(lay, packed, corr_pos, M, m_layout, d, e, nullptr, normed, normed_s, conf, s, rg);
+    std::lock_guard<std::mutex> lock(ss->mu);
+    const int h = d.B / 2;
+    HIPCHK(hipEventRecord(ss->fork, s));
+    HIPCHK(hipStreamWaitEvent(ss->s2, ss->fork, 0));
+    int r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf, s, rg, 0, h);
+    if (r == PDSC_OK)
+        r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf, ss->s2, rg, h, d.B - h);
+    if (r != PDSC_OK) return r;
+    HIPCHK(hipEventRecord(ss->join, ss->s2));
+    HIPCHK(hipStreamWaitEvent(s, ss->join, 0));
     return PDSC_OK;
 }
 
@@ -700,12 +790,18 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     Carve c(ws);
     const FwdBufs f = carve_forward(c, d);
     Ragged rg;
+    SideStream *halves = enc_halves(d, counts != nullptr) ? side_stream() : nullptr;
     if (counts) {
         HIPCHK(launch_ragged_setup(counts, B, cfg->ratio, f.nv, f.sv, s));
         rg.nv = f.nv;
         rg.sv = f.sv;
         if (ragged_order_on()) {
-            HIPCHK(launch_ragged_order(counts, B, f.po, s));
+            if (halves) {  // each half's attention launches order that half's pairs
+                HIPCHK(launch_ragged_order(counts, B / 2, f.po, s));
+                HIPCHK(launch_ragged_order(counts + B / 2, B - B / 2, f.po + B / 2, s));
+            } else {
+                HIPCHK(launch_ragged_order(counts, B, f.po, s));
+            }
             rg.po = f.po;
         }
     }
@@ -727,7 +823,7 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder(lay, packed, corr_pos, f.M, mlay, d, f.enc, nullptr, f.normed, f.normed_s, f.conf, s, rg));
+    RET_IF(run_encoder_fwd(lay, packed, corr_pos, f.M, mlay, d, f.enc, f.normed, f.normed_s, f.conf, s, rg, halves));
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s, rg));

@@ -1764,6 +1764,15 @@ static PwMsg msg3(const LayerOff &l) { return PwMsg{l.fc0, l.fc3, l.fc6}; }
 // attn_pw2 wherever pw2 runs and the attention has one key split (knob
 // PDSC_FUSE=0 keeps the two launches; measurement only).
 static AttnGridH3 fused_grid(int B, int N) { return attention_h3_grid<PW2_W>(B, N, att_target() * 4 / PW2_W); }
+// the fused launches' grid: one key split always (attention_fused chose the plan
+// on the whole batch; a part of it -- run_encoder_part's halves -- keeps it)
+static AttnGridH3 fused_launch_grid(int B, int N) {
+    AttnGridH3 g = fused_grid(B, N);
+    const int nst = (N + H3_TILE - 1) / H3_TILE;
+    g.sps = nst;
+    g.nsplit = 1;
+    return g;
+}
 bool attention_fused(int B, int N, bool f32) {
     static const bool off = [] {
         const char *e = getenv("PDSC_FUSE");
@@ -1777,7 +1786,7 @@ bool attention_fused(int B, int N, bool f32) {
 hipError_t launch_attn_pw2(const float *packed, const PackLayout &lay, int layer, const void *q, const void *k,
                            const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N, int Npad,
                            float *feat, void *qo, void *ko, void *vo, float *vexp_out, hipStream_t s, Ragged rg) {
-    AttnGridH3 g = fused_grid(B, N);
+    AttnGridH3 g = fused_launch_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
     g.rev = rg.po ? 0 : zigzag_rev(layer);  // (ragged batches keep their longest-first order)
@@ -1800,7 +1809,7 @@ hipError_t launch_attn_pw2_last(const float *packed, const PackLayout &lay, cons
                                 const void *v, const float *vexp_in, const float *M, bool m_packed, int B, int N,
                                 int Npad, const float *feat, float *feat_out, float *normed, _Float16 *normed_s,
                                 float *conf, hipStream_t s, Ragged rg) {
-    AttnGridH3 g = fused_grid(B, N);
+    AttnGridH3 g = fused_launch_grid(B, N);
     g.nv = rg.nv;
     g.po = rg.po;
     g.rev = rg.po ? 0 : zigzag_rev(lay.L - 1);

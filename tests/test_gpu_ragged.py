@@ -110,6 +110,21 @@ def test_ragged_uniform_equals_batched(gpu_device):
     assert torch.equal(T, T2) and torch.equal(L, L2)
 
 
+@pytest.mark.parametrize("B", [64, 65])
+def test_ragged_halves_equal_uniform(B, gpu_device):
+    """From 32 pairs a ragged batch runs the fused encoder as two half batches on
+    two streams (api.hip: run_encoder_fwd; an odd B splits 32 / 33); with every
+    count N it is bitwise the uniform forward, which stays on one stream."""
+    from pointdsc_amd import kernels
+    from pointdsc_amd.synthetic import synthetic_batch
+    m, _ = _model(gpu_device)
+    d = synthetic_batch(B, 1000, seed=83)
+    corr, src, tgt = (torch.from_numpy(d[k]).to(gpu_device) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+    T, L = m.forward_batched(corr, src, tgt)
+    T2, L2 = kernels.forward_ragged(m.pdsc_config(), m.packed_weights(), corr, src, tgt, [1000] * B)
+    assert torch.equal(T, T2) and torch.equal(L, L2)
+
+
 @pytest.mark.parametrize("B", [8, 130])
 def test_ragged_vs_single_forwards(B, gpu_device):
     """forward_list over B pairs of N in [600, 1400] (B = 130: the fused
