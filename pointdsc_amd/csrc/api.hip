@@ -174,7 +174,8 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
     const bool m_packed = m_layout == M_PACKED;
     const bool w64 = d.w64 && !d.fuse;
     if (w64 && m_layout != M_PACKED) return fail(PDSC_ERR_ARG, "M layout %d for this plan", m_layout);
-    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg));
+    HIPCHK(launch_pw_first(packed, lay, corr_pos, d.f32, d.B, d.N, d.Npad, e.feat, e.q, e.k, e.v, e.vexp, s, rg,
+                           d.fuse));
     if (d.fuse) {  // every layer fused (0 .. L-2 with the next layer's PointCN/QKV, Q/K/V alternating between the two sets)
         _Float16 *q = e.q, *k = e.k, *v = e.v, *q2 = e.q2, *k2 = e.k2, *v2 = e.v2;
         float *vx = e.vexp, *vx2 = e.vexp2;
@@ -220,15 +221,19 @@ int run_encoder(const PackLayout &lay, const float *packed, const float *corr_po
     return PDSC_OK;
 }
 
-// Ragged batches run the fused encoder as two half batches of pairs on two
-// streams (the caller's and a per-device side stream, forked and joined by
-// events), so one half's launches fill the other's dispatch tails: a ragged
+// Ragged batches run the fused encoder as P parts of the batch (contiguous pair
+// ranges of equal pair counts), each on its own
+// stream -- the caller's and P - 1 per-device side streams, forked and joined
+// by events -- so one part's launches fill the others' dispatch tails: a ragged
 // batch's attention launches end in a tail of a few long workgroups per XCD
-// (DESIGN.md §7).  Pairs are independent through the encoder, so each half is
+// (DESIGN.md §7).  Pairs are independent through the encoder, so each part is
 // the same arithmetic on its own pointer range (bitwise equal results).
-// 128 pairs, N in [700, 1300]: 4.54 -> 4.12 ms per forward; uniform batches
-// (two full rounds of workgroups, no tail to fill) measured 3.77 -> 3.83 ms, so
-// they stay on one stream.  Knob PDSC_ENC_HALVES: 0 never, 1 uniform batches too.
+// 128 pairs, N in [700, 1300], two halves: 4.54 -> 4.12 ms per forward (three
+// parts 4.23, four 4.32 vs two 4.19 on another box); uniform batches (two full
+// rounds of workgroups, no tail to fill) measured 3.77 -> 3.83 ms, so they stay
+// on one stream.  Knobs: PDSC_ENC_HALVES 0 never, 1 uniform batches too;
+// PDSC_ENC_PARTS P in [2, 4] (default 2).  Every part keeps the whole batch's
+// plan (the fused launches' one key split, pw2_first's layouts).
 static int enc_halves_mode() {
     static const int v = [] {
         const char *e = getenv("PDSC_ENC_HALVES");
@@ -236,15 +241,49 @@ static int enc_halves_mode() {
     }();
     return v;
 }
+constexpr int ENC_MAX_PARTS = 4;
+static int enc_parts() {
+    static const int v = [] {
+        const char *e = getenv("PDSC_ENC_PARTS");
+        const int p = e ? atoi(e) : 2;
+        return std::min(std::max(p, 2), ENC_MAX_PARTS);
+    }();
+    return v;
+}
+// Parts of equal pair counts; A/B knob PDSC_ENC_BAL=1: parts of equal work
+// sum(n^2) instead (measured slower: 128 pairs, N in [700, 1300], 4.150 / 4.159
+// vs 4.021 / 4.056 ms per forward, one stream 4.423 / 4.437).
+static bool enc_work_balanced() {
+    static const bool on = [] {
+        const char *e = getenv("PDSC_ENC_BAL");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 static bool enc_halves(const Dims &d, bool ragged) {
     const int mode = enc_halves_mode();
-    return d.fuse && d.B >= 32 && (mode == 2 || (mode == 1 && ragged));
+    return d.fuse && d.B >= 16 * enc_parts() && (mode == 2 || (mode == 1 && ragged));
+}
+// Part boundaries bounds[0 .. P]: bounds[i] = the first pair whose work prefix
+// reaches i/P of the total (counts: HOST sizes, or NULL for a uniform batch).
+static void enc_bounds(const int32_t *counts, int B, int P, int *bounds) {
+    std::vector<double> pre(B + 1, 0.0);
+    for (int b = 0; b < B; ++b) pre[b + 1] = pre[b] + (counts ? (double)counts[b] * counts[b] : 1.0);
+    bounds[0] = 0;
+    bounds[P] = B;
+    for (int i = 1; i < P; ++i) {
+        const double goal = pre[B] * i / P;
+        int h = bounds[i - 1] + 1;
+        while (h < B - (P - i) && std::abs(pre[h + 1] - goal) < std::abs(pre[h] - goal)) ++h;
+        bounds[i] = h;
+    }
 }
 
 struct SideStream {
     std::mutex mu;  // one fork / join enqueued at a time per device
-    hipStream_t s2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t s2[ENC_MAX_PARTS - 1] = {};
+    hipEvent_t fork = nullptr, join[ENC_MAX_PARTS - 1] = {};
+    bool ok = false;
 };
 static SideStream *side_stream() {
     static SideStream ss[64];
@@ -253,12 +292,15 @@ static SideStream *side_stream() {
     SideStream &x = ss[dev];
     static std::mutex create_mu;
     std::lock_guard<std::mutex> lock(create_mu);
-    if (!x.join) {  // all three or none (a failure leaves the forward on one stream)
-        if (!x.s2 && hipStreamCreateWithFlags(&x.s2, hipStreamNonBlocking) != hipSuccess) x.s2 = nullptr;
-        if (x.s2 && !x.fork && hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) x.fork = nullptr;
-        if (x.fork && hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) x.join = nullptr;
+    if (!x.ok) {  // all or none (a failure leaves the forward on one stream)
+        bool ok = x.fork || hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < ENC_MAX_PARTS - 1; ++i) {
+            if (!x.s2[i]) ok = hipStreamCreateWithFlags(&x.s2[i], hipStreamNonBlocking) == hipSuccess;
+            if (ok && !x.join[i]) ok = hipEventCreateWithFlags(&x.join[i], hipEventDisableTiming) == hipSuccess;
+        }
+        x.ok = ok;
     }
-    return x.join ? &x : nullptr;
+    return x.ok ? &x : nullptr;
 }
 
 // The fused plan's encoder over pairs [b0, b0 + nb): every per-pair pointer
@@ -289,23 +331,26 @@ static int run_encoder_part(const PackLayout &lay, const float *packed, const fl
                        conf + (size_t)b0 * d.N, s, rh);
 }
 
-// run_encoder for the forward: the fused plan as two concurrent halves given a
-// side stream ss (enc_halves; rg.po, when set, must then order each half's
-// pairs on its own: launch_ragged_order per half), else run_encoder itself.
+// run_encoder for the forward: the fused plan as P concurrent parts given side
+// streams ss and the part boundaries (enc_halves / enc_bounds; rg.po, when set,
+// must then order each part's pairs on its own: launch_ragged_order per part),
+// else run_encoder itself.
 static int run_encoder_fwd(const PackLayout &lay, const float *packed, const float *corr_pos, const float *M,
                            int m_layout, const Dims &d, const EncBufs &e, float *normed, _Float16 *normed_s,
-                           float *conf, hipStream_t s, Ragged rg, SideStream *ss) {
+                           float *conf, hipStream_t s, Ragged rg, SideStream *ss, const int *bounds, int P) {
     if (!ss) return run_encoder(lay, packed, corr_pos, M, m_layout, d, e, nullptr, normed, normed_s, conf, s, rg);
     std::lock_guard<std::mutex> lock(ss->mu);
-    const int h = d.B / 2;
     HIPCHK(hipEventRecord(ss->fork, s));
-    HIPCHK(hipStreamWaitEvent(ss->s2, ss->fork, 0));
-    int r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf, s, rg, 0, h);
-    if (r == PDSC_OK)
-        r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf, ss->s2, rg, h, d.B - h);
-    if (r != PDSC_OK) return r;
-    HIPCHK(hipEventRecord(ss->join, ss->s2));
-    HIPCHK(hipStreamWaitEvent(s, ss->join, 0));
+    for (int i = 1; i < P; ++i) HIPCHK(hipStreamWaitEvent(ss->s2[i - 1], ss->fork, 0));
+    for (int i = 0; i < P; ++i) {
+        const int r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf,
+                                       i ? ss->s2[i - 1] : s, rg, bounds[i], bounds[i + 1] - bounds[i]);
+        if (r != PDSC_OK) return r;
+    }
+    for (int i = 1; i < P; ++i) {
+        HIPCHK(hipEventRecord(ss->join[i - 1], ss->s2[i - 1]));
+        HIPCHK(hipStreamWaitEvent(s, ss->join[i - 1], 0));
+    }
     return PDSC_OK;
 }
 
@@ -791,17 +836,16 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     const FwdBufs f = carve_forward(c, d);
     Ragged rg;
     SideStream *halves = enc_halves(d, counts != nullptr) ? side_stream() : nullptr;
+    const int parts = halves ? enc_parts() : 1;
+    int bounds[ENC_MAX_PARTS + 1] = {0, B};
+    if (halves) enc_bounds(enc_work_balanced() ? counts : nullptr, B, parts, bounds);
     if (counts) {
         HIPCHK(launch_ragged_setup(counts, B, cfg->ratio, f.nv, f.sv, s));
         rg.nv = f.nv;
         rg.sv = f.sv;
-        if (ragged_order_on()) {
-            if (halves) {  // each half's attention launches order that half's pairs
-                HIPCHK(launch_ragged_order(counts, B / 2, f.po, s));
-                HIPCHK(launch_ragged_order(counts + B / 2, B - B / 2, f.po + B / 2, s));
-            } else {
-                HIPCHK(launch_ragged_order(counts, B, f.po, s));
-            }
+        if (ragged_order_on()) {  // each part's attention launches order that part's pairs
+            for (int i = 0; i < parts; ++i)
+                HIPCHK(launch_ragged_order(counts + bounds[i], bounds[i + 1] - bounds[i], f.po + bounds[i], s));
             rg.po = f.po;
         }
     }
@@ -823,7 +867,8 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
         HIPCHK(launch_compat(src, tgt, d.B, d.N, sigma_d, f.M, s, rg));
     STAGE(1);
     // a2-a4 (:155-156, :171)
-    RET_IF(run_encoder_fwd(lay, packed, corr_pos, f.M, mlay, d, f.enc, f.normed, f.normed_s, f.conf, s, rg, halves));
+    RET_IF(run_encoder_fwd(lay, packed, corr_pos, f.M, mlay, d, f.enc, f.normed, f.normed_s, f.conf, s, rg, halves,
+                           bounds, parts));
     STAGE(2);
     // a5 (:174)
     HIPCHK(launch_local_max(src, f.conf, d.B, d.N, cfg->nms_radius, f.lm, s, rg));

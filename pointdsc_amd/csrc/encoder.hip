@@ -1883,10 +1883,10 @@ static bool pw_qkv_split(int B, int Npad) {
 
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
                            int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
-                           Ragged rg) {
+                           Ragged rg, bool fused) {
     if (lay.in_dim > IN_LIMIT) return hipErrorInvalidValue;
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
-    if (use_pw2(B, Npad, f32)) {
+    if (fused || use_pw2(B, Npad, f32)) {  // the fused plan's layouts (a part of a batch: the batch's plan)
         const W2Sched S = sched_qkv(W2Sched{}, dense4(lay.layer[0]));
         hipLaunchKernelGGL(pw2_first_kernel, dim3((Npad + PW2_PTS - 1) / PW2_PTS, B), dim3(PW2_W * 64), PW2_LDS, s,
                            packed, S, lay.l0_w, lay.l0_b, dense4(lay.layer[0]), corr_pos, lay.in_dim, N, Npad, feat, Q, K,

@@ -204,9 +204,10 @@ hipError_t launch_attn_combine(const float *opart, const float *ml, bool f32, in
                                int nsplit, float *msg, hipStream_t s);
 
 // Pointwise chains (one workgroup per PT points); q, k, v in launch_attention's layouts.
+// fused: the batch runs the fused plan (attention_fused), whatever B this call covers.
 hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const float *corr_pos, bool f32, int B,
                            int N, int Npad, float *feat, void *q, void *k, void *v, float *vexp, hipStream_t s,
-                           Ragged rg = {});
+                           Ragged rg = {}, bool fused = false);
 // H3 split partials (nsplit) -> one combined split (opart1 [B][Npad][CH] in the
 // h3 tiling, ml1 = (0, 1)) that pw_mid / pw_last read with nsplit = 1 (small
 // batches: combine16's per-thread load chain is the pointwise launch's latency).

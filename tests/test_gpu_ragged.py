@@ -110,11 +110,14 @@ def test_ragged_uniform_equals_batched(gpu_device):
     assert torch.equal(T, T2) and torch.equal(L, L2)
 
 
-@pytest.mark.parametrize("B", [64, 65])
+@pytest.mark.parametrize("B", [64, 128])
 def test_ragged_halves_equal_uniform(B, gpu_device):
-    """From 32 pairs a ragged batch runs the fused encoder as two half batches on
-    two streams (api.hip: run_encoder_fwd; an odd B splits 32 / 33); with every
-    count N it is bitwise the uniform forward, which stays on one stream."""
+    """From 32 pairs on the fused plan a ragged batch runs the encoder as two half
+    batches on two streams (api.hip: run_encoder_fwd), each keeping the whole
+    batch's plan (at 64 pairs a half of 32 alone would take the unfused chains);
+    with every count N it is bitwise the uniform forward, which stays on one
+    stream.  (Odd splits: test_ragged_vs_single_forwards[130] and the other
+    ragged tests, which all run with the halves.)"""
     from pointdsc_amd import kernels
     from pointdsc_amd.synthetic import synthetic_batch
     m, _ = _model(gpu_device)
