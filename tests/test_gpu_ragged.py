@@ -128,6 +128,29 @@ def test_ragged_halves_equal_uniform(B, gpu_device):
     assert torch.equal(T, T2) and torch.equal(L, L2)
 
 
+def test_ragged_halves_graph_capture(gpu_device):
+    """The halves' event fork / join onto the side stream records into a HIP
+    graph: a captured ragged forward (128 pairs, N in [700, 1300]: the fused
+    plan, bench.py's ragged leg) replays to bitwise the eager results."""
+    from pointdsc_amd import kernels
+    m, _ = _model(gpu_device)
+    rng = np.random.RandomState(5)
+    sizes = rng.randint(700, 1301, size=128).tolist()
+    ds = _datas(_pairs(sizes, seed=84), gpu_device)
+    corr, counts = kernels.pad_pairs([d["corr_pos"] for d in ds])
+    src, _ = kernels.pad_pairs([d["src_keypts"] for d in ds])
+    tgt, _ = kernels.pad_pairs([d["tgt_keypts"] for d in ds])
+    cfg, pk = m.pdsc_config(), m.packed_weights()
+    T, L = kernels.forward_ragged(cfg, pk, corr, src, tgt, counts, check_range=False)  # eager (and warm)
+    torch.cuda.synchronize(gpu_device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        Tg, Lg = kernels.forward_ragged(cfg, pk, corr, src, tgt, counts, check_range=False)
+    g.replay()
+    torch.cuda.synchronize(gpu_device)
+    assert torch.equal(T, Tg) and torch.equal(L, Lg)
+
+
 @pytest.mark.parametrize("B", [8, 130])
 def test_ragged_vs_single_forwards(B, gpu_device):
     """forward_list over B pairs of N in [600, 1400] (B = 130: the fused
