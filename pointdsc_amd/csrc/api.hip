@@ -285,19 +285,26 @@ struct SideStream {
     hipEvent_t fork = nullptr, join[ENC_MAX_PARTS - 1] = {};
     bool ok = false;
 };
-static SideStream *side_stream() {
+// The side streams of the device that stream s runs on (the current device for
+// the legacy default stream), created there on first use.
+static SideStream *side_stream(hipStream_t s) {
     static SideStream ss[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    hipDevice_t dev = 0;
+    if (!s || hipStreamGetDevice(s, &dev) != hipSuccess)
+        if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (dev < 0 || dev >= 64) return nullptr;
     SideStream &x = ss[dev];
     static std::mutex create_mu;
     std::lock_guard<std::mutex> lock(create_mu);
     if (!x.ok) {  // all or none (a failure leaves the forward on one stream)
+        int cur = dev;
+        if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) return nullptr;
         bool ok = x.fork || hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < ENC_MAX_PARTS - 1; ++i) {
             if (!x.s2[i]) ok = hipStreamCreateWithFlags(&x.s2[i], hipStreamNonBlocking) == hipSuccess;
             if (ok && !x.join[i]) ok = hipEventCreateWithFlags(&x.join[i], hipEventDisableTiming) == hipSuccess;
         }
+        if (cur != dev) (void)hipSetDevice(cur);
         x.ok = ok;
     }
     return x.ok ? &x : nullptr;
@@ -835,7 +842,7 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     Carve c(ws);
     const FwdBufs f = carve_forward(c, d);
     Ragged rg;
-    SideStream *halves = enc_halves(d, counts != nullptr) ? side_stream() : nullptr;
+    SideStream *halves = enc_halves(d, counts != nullptr) ? side_stream(s) : nullptr;
     const int parts = halves ? enc_parts() : 1;
     int bounds[ENC_MAX_PARTS + 1] = {0, B};
     if (halves) enc_bounds(enc_work_balanced() ? counts : nullptr, B, parts, bounds);
