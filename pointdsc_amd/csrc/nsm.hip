@@ -18,6 +18,13 @@
 
 namespace pdsc {
 
+// NSM A/B build knob: 1 (default) the T build on packed fp32 (source, target)
+// pairs and the power iterate's norm through the wave-uniform cr_sqrt; 0 the
+// scalar T build and sqrtf (the same bits either way)
+#ifndef NSM_PK_TBUILD
+#define NSM_PK_TBUILD 1
+#endif
+
 // ------------------------------------------------------------------ a6 kNN
 // dist[b][s][j] = 2 - 2 * <normed[seed_s], normed[j]>   (models/common.py:58-60)
 // on the fp16 matrix cores with the 3-product split of attention_h3.hpp
@@ -573,7 +580,16 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
             acc23 = __builtin_elementwise_fma(f32x2{trow[c + 2], trow[c + 3]}, f32x2{vv[2], vv[3]}, acc23);
         }
         float nv = (acc01[0] + acc01[1]) + (acc23[0] + acc23[1]);   // (T v)_a  (bmm, :352)
-        const float nrm = sqrtf(wave_sum_dpp(nv * nv));  // no LDS round trip per iterate
+        // no LDS round trip per iterate; every lane holds the same sum, so the
+        // square root branches wave-uniformly: the fma-corrected cr_sqrt (the
+        // same correctly rounded value) where it is exact, sqrtf below 2^-96
+#if NSM_PK_TBUILD
+        const float ss = __builtin_bit_cast(
+            float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, wave_sum_dpp(nv * nv))));
+        const float nrm = ss >= 0x1p-96f ? cr_sqrt(ss) : sqrtf(ss);
+#else
+        const float nrm = sqrtf(wave_sum_dpp(nv * nv));
+#endif
         nv = nv / (nrm + 1e-6f);                              // :353
         const bool close = (a >= k) || (fabsf(nv - v) <= 1e-8f + 1e-5f * fabsf(v));  // allclose (:354)
         if (__all(close)) flags |= 1u << t;
@@ -596,10 +612,6 @@ PDSC_DEV unsigned power_iterate(const float *trow_lds, int tstride, int k, int T
 // same wave runs the power iteration.  No workgroup barriers: waves are
 // independent.
 constexpr int NSM_PSTR = 8;  // floats per neighbour in the LDS coordinate table
-// T build on packed fp32 (source, target) pairs; 0: the scalar form (A/B builds)
-#ifndef NSM_PK_TBUILD
-#define NSM_PK_TBUILD 1
-#endif
 // cr_sqrt / cr_div (pdsc_common.hpp) on two lanes' worth of operands: the
 // fma corrections as v_pk_fma_f32, the same operations per component.
 PDSC_DEV f32x2 cr_sqrt2(f32x2 x) {
