@@ -21,7 +21,9 @@ stream the kernels run on:
   stages        -- per-stage ms of the headline forward (pdsc_forward_timing events)
   roofline_sm   -- SURVEY 8(f) row 3: the SM baseline's matrix-vector product at N=9000 (M past the
                    Infinity Cache), HBM bound
-  single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph
+  single_pair   -- configs[1] literally: one N=1000 pair per forward, eager and as a HIP graph,
+                   per-stage split, and the drop-in PointDSC.forward's host wall
+  single_pair_5k -- the same at N=5000: the reference drivers' own call (bs = 1, N ~ 5000)
   ragged        -- one call over P pairs of mixed N (0.7-1.3 N), the evaluation loop's shape
 Each roofline's `traffic` is the HBM bytes per launch of the same kernel at the
 same launch shape from the committed rocprofv3 profile (profiles/traffic_current.json).
@@ -342,10 +344,14 @@ def main():
         plan.run(corr, src, tgt)
     torch.cuda.synchronize(dev)
     L.pdsc_forward_timing(None, 0, None)
+    own_elapsed = elapsed
+    elapsed_min = elapsed
     if grp:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        tmin = torch.tensor([own_elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tmin, op=torch.distributed.ReduceOp.MIN)
+        elapsed, elapsed_min = float(t.item()), float(tmin.item())
     ms_per_step = elapsed / args.steps * 1e3
     value = world * P * N * args.steps / elapsed
     # the fp16 range guard's marks of the last timed step (include/pdsc.h; after the clock)
@@ -359,8 +365,10 @@ def main():
     from pointdsc_amd.evaluate import THRESHOLDS, pair_stats
     gtT, gtL = torch.from_numpy(data["gt_trans"]).to(dev), torch.from_numpy(data["gt_labels"]).to(dev)
     rows = pair_stats(plan.trans, gtT, plan.labels, gtL, *THRESHOLDS[args.preset])
+    rows = torch.cat([rows, torch.tensor(mine, dtype=rows.dtype, device=rows.device)[:, None]], 1)
     allrows = pdist.gather_rows(rows, P * world, device=dev)
     recall = float(allrows[:, 0].mean())
+    pair_ids_ok = sorted(allrows[:, -1].long().tolist()) == list(range(P * world))
 
     result = None
     if rank == 0:
@@ -525,35 +533,50 @@ def main():
                            "sm_pair_ms": round(sm_ms, 3)}
             del Mm, vv
 
-        # ---- configs[1] literally: a single N pair per forward (latency), eager and graph-replayed
-        d1 = synthetic_batch(1, N, seed=7000 + rank, preset=args.preset)
-        c1, s1, t1 = (torch.from_numpy(d1[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
-        plan1 = kernels.ForwardPlan(cfg, packed, 1, N, dev)
-        e_ms = event_time(lambda: plan1.run(c1, s1, t1), 20, stream)
-        plan1.capture(c1, s1, t1)
-        g_ms = event_time(lambda: plan1.run(c1, s1, t1), 50, stream)
-        del plan1
-        # the drop-in call as the reference's drivers make it (evaluation/test_3DMatch.py:52-53,
-        # demo_registration.py:117): model(data) per pair at bs = 1, host wall time of the whole
-        # call -- argument checks, packed-weight change check, workspace, ~48 launches and the
-        # synchronising fp16 range-guard read -- one call after the other
-        data1 = {"corr_pos": c1, "src_keypts": s1, "tgt_keypts": t1, "testing": True}
-        for _ in range(5):
-            model(data1)
-        torch.cuda.synchronize(dev)
-        packs0, walls = model.pack_count, []
-        for _ in range(50):
-            t0 = time.perf_counter()
-            model(data1)
-            walls.append((time.perf_counter() - t0) * 1e3)
-        single = {"num_corr": N, "eager_ms": round(e_ms, 4), "graph_ms": round(g_ms, 4),
-                  "graph_correspondences_per_s": round(N / (g_ms * 1e-3), 1),
-                  "drop_in_ms": round(float(np.mean(walls)), 4), "drop_in_median_ms": round(float(np.median(walls)), 4),
-                  "drop_in_over_eager": round(float(np.mean(walls)) / e_ms, 3),
-                  "drop_in_repacks": model.pack_count - packs0,
-                  "drop_in_note": "PointDSC.forward({'testing': True, ...}) at bs = 1, host wall per call over 50 "
-                                  "calls (range-guard read included); eager_ms / graph_ms: device time of "
-                                  "ForwardPlan.run by HIP events"}
+        # ---- configs[1] literally: a single N pair per forward (latency), eager and graph-replayed;
+        # and the reference drivers' own call at N = 5000 (configs[2] / [4]: evaluation/test_3DMatch.py:53,
+        # test_KITTI.py:75 run model(data) once per pair at bs = 1 with N ~ 5000)
+        def single_leg(Ns, seed, n_drop):
+            d1 = synthetic_batch(1, Ns, seed=seed, preset=args.preset)
+            c1, s1, t1 = (torch.from_numpy(d1[k]).to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts"))
+            plan1 = kernels.ForwardPlan(cfg, packed, 1, Ns, dev)
+            e_ms = event_time(lambda: plan1.run(c1, s1, t1), 20, stream)
+            sev1 = EventPool(5 * (len(STAGES) + 1))  # per-stage device time of 5 more eager forwards
+            L.pdsc_forward_timing(sev1.ev, sev1.n, ctypes.byref(sev1.count))
+            for _ in range(5):
+                plan1.run(c1, s1, t1)
+            torch.cuda.synchronize(dev)
+            L.pdsc_forward_timing(None, 0, None)
+            st1, _ = sev1.stage_means()
+            plan1.capture(c1, s1, t1)
+            g_ms = event_time(lambda: plan1.run(c1, s1, t1), 50, stream)
+            del plan1
+            # the drop-in call as the reference's drivers make it (evaluation/test_3DMatch.py:52-53,
+            # demo_registration.py:117): model(data) per pair at bs = 1, host wall time of the whole
+            # call -- argument checks, packed-weight change check, workspace, ~48 launches and the
+            # synchronising fp16 range-guard read -- one call after the other
+            data1 = {"corr_pos": c1, "src_keypts": s1, "tgt_keypts": t1, "testing": True}
+            for _ in range(5):
+                model(data1)
+            torch.cuda.synchronize(dev)
+            packs0, walls = model.pack_count, []
+            for _ in range(n_drop):
+                t0 = time.perf_counter()
+                model(data1)
+                walls.append((time.perf_counter() - t0) * 1e3)
+            return {"num_corr": Ns, "eager_ms": round(e_ms, 4), "graph_ms": round(g_ms, 4),
+                    "graph_correspondences_per_s": round(Ns / (g_ms * 1e-3), 1),
+                    "stage_ms": {k: round(v, 4) for k, v in st1.items()},
+                    "drop_in_ms": round(float(np.mean(walls)), 4), "drop_in_median_ms": round(float(np.median(walls)), 4),
+                    "drop_in_over_eager": round(float(np.mean(walls)) / e_ms, 3),
+                    "drop_in_correspondences_per_s": round(Ns / (float(np.mean(walls)) * 1e-3), 1),
+                    "drop_in_repacks": model.pack_count - packs0,
+                    "drop_in_note": f"PointDSC.forward({{'testing': True, ...}}) at bs = 1, host wall per call over "
+                                    f"{n_drop} calls (range-guard read included); eager_ms / graph_ms / stage_ms: "
+                                    f"device time of ForwardPlan.run by HIP events"}
+
+        single = single_leg(N, 7000 + rank, 50)
+        single_5k = single_leg(5000, 7500 + rank, 20) if args.path_n > 0 else None
 
         # ---- a ragged batch (pdsc_forward_testing_ragged): P pairs of N_b ~ U[0.7 N, 1.3 N],
         # the evaluation loop's mixed sizes in one call (datasets/ThreeDMatch.py:268-290)
@@ -654,11 +677,19 @@ def main():
                        "parallelism": f"dp{world} (independent pairs)"},
             "scan_pairs_per_s": round(world * P * args.steps / elapsed, 2),
             "synthetic_recall": recall, "pairs_gathered": int(allrows.shape[0]),
+            # self-check of the multi-rank run (the driver's SCALE runs): the process group's size,
+            # the spread of the ranks' own timed regions, and every global pair gathered once
+            "distributed": {"world_size": torch.distributed.get_world_size() if grp else 1,
+                            "backend": torch.distributed.get_backend() if grp else None,
+                            "rank_ms_per_step": {"min": round(elapsed_min / args.steps * 1e3, 4),
+                                                 "max": round(ms_per_step, 4)},
+                            "pairs_expected": P * world, "pairs_gathered": int(allrows.shape[0]),
+                            "pair_ids_ok": pair_ids_ok},
             "range_marked_pairs": range_marked,
             "roofline": roofline, "roofline_hbm": roofline_hbm, "roofline_hbm_dense": roofline_hbm_dense,
             "roofline_path": roofline_path,
             "roofline_sm": roofline_sm,
-            "stages_ms": stages, "single_pair": single, "ragged": ragged, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
+            "stages_ms": stages, "single_pair": single, "single_pair_5k": single_5k, "ragged": ragged, "exact_f32": exact, "cpu_baseline": cpu, "parity": parity,
         }
         print(json.dumps(result), flush=True)
     if grp:

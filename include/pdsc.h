@@ -178,6 +178,12 @@ int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_event
  * *count += 8, while *count + 8 <= capacity.  Capacity 0 disables.           */
 #define PDSC_FORWARD_STAGES 7
 int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *count);
+/* Test hook (no reference counterpart): the small-batch pw_mid's K / V
+ * workgroups of the Q / K / V split sleep `loops` x 127 x 64 cycles before
+ * their first load (0: off, the default).  A per-thread setting like the
+ * timing hooks; tests/test_gpu_parity.py uses it to pin that the split's
+ * readers of the residual rows cannot see the Q workgroup's new rows.       */
+int32_t pdsc_diag_qkv_delay(int32_t loops);
 
 /* ------------------------------------------------------- a5 seeds ----------
  * pick_seeds: radius NMS on the confidences then the top-S of

@@ -34,9 +34,9 @@ from torch.nn.modules import module as _nn_module
 from . import _lib, kernels
 
 # Bumped whenever ANY module registers (or replaces) a parameter, buffer or
-# sub-module -- e.g. ``model.encoder.layer0.weight = nn.Parameter(...)``: the
-# packed weights of every PointDSC are then rebuilt on its next forward.  (New
-# modules bump it while they are built; an evaluation loop builds none.)
+# sub-module -- e.g. ``model.encoder.layer0.weight = nn.Parameter(...)``: every
+# PointDSC then compares its own packed tensors' identities on its next forward
+# and re-packs only if one of ITS tensors was replaced (PointDSC.packed_weights).
 _REGISTRATION_EPOCH = [0]
 
 
@@ -50,6 +50,20 @@ _nn_module.register_module_module_registration_hook(_bump_epoch)
 
 # workspaces up to this size stay cached per stream between forwards
 _WS_CACHE_LIMIT = 256 << 20
+
+_HIP = []
+
+
+def _hip():
+    """libamdhip64 (hipMemcpyAsync into the pinned range-flag word, hipStreamSynchronize)."""
+    if not _HIP:
+        h = ctypes.CDLL("libamdhip64.so")
+        h.hipMemcpyAsync.restype = ctypes.c_int
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        h.hipStreamSynchronize.restype = ctypes.c_int
+        h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        _HIP.append(h)
+    return _HIP[0]
 
 
 class NonLocalBlock(nn.Module):
@@ -163,8 +177,13 @@ class PointDSC(nn.Module):
 
     def _packable(self, cfg):
         """{state_dict key: tensor} the kernels' blob is packed from (pdsc_param_name order)."""
-        L = _lib.load()
-        names = [L.pdsc_param_name(ctypes.byref(cfg), i).decode() for i in range(L.pdsc_param_count(ctypes.byref(cfg)))]
+        cache = self.__dict__.setdefault("_names_cache", {})
+        lkey = (cfg.in_dim, cfg.num_layers, cfg.num_channels)
+        names = cache.get(lkey)
+        if names is None:
+            L = _lib.load()
+            names = cache[lkey] = [L.pdsc_param_name(ctypes.byref(cfg), i).decode()
+                                   for i in range(L.pdsc_param_count(ctypes.byref(cfg)))]
         named = dict(self.named_parameters())
         named.update(self.named_buffers())
         missing = [n for n in names if n not in named]
@@ -177,45 +196,82 @@ class PointDSC(nn.Module):
         views share their base's version counter, so any in-place edit of any of
         them (optimizer steps under no_grad, ``copy_`` in ``load_state_dict``,
         ``mul_``...) bumps ``flat._version`` -- the per-forward change check is one
-        integer compare instead of walking 358 tensors (1.4 ms per call).
-        Values, names, shapes and requires_grad are unchanged; the Parameter
-        objects are new ones (state_dict() keys and contents are the same)."""
+        integer compare instead of walking 358 tensors (60-130 us of Python per
+        call).  Every Parameter / buffer keeps its Python object (its contents are
+        swapped in place by ``torch.utils.swap_tensors``), so optimizers, hooks and
+        references taken before the first forward stay live; values, names,
+        shapes, requires_grad and .grad are unchanged.  The flat buffer is built
+        outside inference mode, so a first forward under ``torch.inference_mode()``
+        leaves ordinary tensors behind.  Returns None (no flattening: the caller
+        falls back to the per-tensor check) when a tensor is not a float32 device
+        tensor or cannot be swapped (e.g. it has weak references)."""
         ts = list(tensors.values())
         dev = ts[0].device
         if not all((t.is_cuda or not device_only) and t.device == dev and t.dtype == torch.float32 for t in ts):
             return None  # pack_weights raises the precise error (CPU tensor, dtype)
-        flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        off = 0
-        for name, t in tensors.items():
-            view = flat[off:off + t.numel()].view(t.shape)
-            off += t.numel()
-            owner, _, leaf = name.rpartition(".")
-            mod = self.get_submodule(owner) if owner else self
-            if leaf in mod._parameters:  # plain dict writes: no registration hook fires
-                mod._parameters[leaf] = nn.Parameter(view, requires_grad=t.requires_grad)
-            else:
-                mod._buffers[leaf] = view
+        with torch.inference_mode(False), torch.no_grad():
+            flat = torch.cat([t.detach().reshape(-1) for t in ts])
+            news, off = [], 0
+            for t in ts:
+                view = flat[off:off + t.numel()].view(t.shape)
+                off += t.numel()
+                if isinstance(t, nn.Parameter):
+                    new = nn.Parameter(view, requires_grad=t.requires_grad)
+                    if t.grad is not None:
+                        new.grad = t.grad
+                else:
+                    new = view.detach()  # shares flat's version counter, not a view object
+                news.append(new)
+            done = []
+            try:
+                for t, new in zip(ts, news):
+                    torch.utils.swap_tensors(t, new)
+                    done.append((t, new))
+            except RuntimeError:
+                for t, new in reversed(done):  # undo: every tensor back on its own storage
+                    torch.utils.swap_tensors(t, new)
+                return None
         return flat
+
+    def _same_tensors(self, st, cfg):
+        """True if this model's packed parameters/buffers are still the objects
+        ``st`` flattened, all still on its flat buffer: a registration elsewhere in
+        the process (another module built) then needs no re-flatten."""
+        if st["flat"] is None:
+            return False
+        lo = st["flat"].data_ptr()
+        hi = lo + st["flat"].numel() * 4
+        cur = self._packable(cfg)
+        return all(cur[n] is t and lo <= t.data_ptr() < hi for n, t in st["tensors"].items())
 
     def packed_weights(self, precision=None) -> torch.Tensor:
         """Kernel-layout weights (one cached packing per precision), re-packed
         when a parameter/buffer changed since: checked per call by the flat
-        buffer's version counter and the module-registration epoch (see
-        ``_flatten``, ``invalidate_packing``)."""
+        buffer's version counter (or, without one, every tensor's) and, after
+        any module registration in the process, by this model's own tensor
+        identities (see ``_flatten``, ``invalidate_packing``)."""
         precision = precision or self.precision
         st = self.__dict__.get("_pack")
         layout = (self.in_dim, self.num_layers, self.num_channels)
-        if st is None or st["epoch"] != _REGISTRATION_EPOCH[0] or st["layout"] != layout:
+        epoch = _REGISTRATION_EPOCH[0]
+        if st is not None and st["epoch"] != epoch and st["layout"] == layout \
+                and self._same_tensors(st, self.pdsc_config(precision)):
+            st["epoch"] = epoch  # the registration was not ours
+        if st is None or st["epoch"] != epoch or st["layout"] != layout:
             cfg = self.pdsc_config(precision)
             tensors = self._packable(cfg)
             flat = self._flatten(tensors)
-            if flat is not None:
-                tensors = self._packable(cfg)  # the views
-            st = self.__dict__["_pack"] = {"epoch": _REGISTRATION_EPOCH[0], "layout": layout, "flat": flat,
-                                           "version": None if flat is None else flat._version,
+            st = self.__dict__["_pack"] = {"epoch": epoch, "layout": layout, "flat": flat,
+                                           "version": flat._version if flat is not None
+                                           else [t._version for t in tensors.values()],
                                            "tensors": tensors, "packed": {}}
-        elif st["flat"] is not None and st["flat"]._version != st["version"]:  # values edited in place
-            st["version"], st["packed"] = st["flat"]._version, {}
+        elif st["flat"] is not None:
+            if st["flat"]._version != st["version"]:  # values edited in place
+                st["version"], st["packed"] = st["flat"]._version, {}
+        else:
+            v = [t._version for t in st["tensors"].values()]
+            if v != st["version"]:
+                st["version"], st["packed"] = v, {}
         if precision not in st["packed"]:
             st["packed"][precision] = kernels.pack_weights(self.pdsc_config(precision), st["tensors"])
             self.__dict__["pack_count"] = self.__dict__.get("pack_count", 0) + 1
@@ -264,6 +320,55 @@ class PointDSC(nn.Module):
                           f"final_trans is NaN and final_labels 0", RuntimeWarning, stacklevel=3)
         return out
 
+    def _forward_one(self, corr_pos, src, tgt):
+        """The drop-in call's path (bs = 1, the reference drivers' shape): one C
+        call on the current stream with the cached workspace, then the fp16 range
+        guard's flag read through a pinned host word (a 4-byte D2H into page-locked
+        memory + one stream synchronisation: 12.6 us idle on MI355X, against 23.6
+        us for pdsc_range_status's copy into pageable memory,
+        tools/dropin_breakdown.py).  Returns None -- the caller then takes the
+        general path, which raises the precise error or re-runs a marked pair in
+        exact fp32 -- when the workspace is not cacheable or the pair is marked."""
+        dev = src.device
+        corr_pos, src, tgt = (kernels._dev(corr_pos, "corr_pos"), kernels._dev(src, "src_keypts"),
+                              kernels._dev(tgt, "tgt_keypts"))
+        cfg, pk = self.pdsc_config(), self.packed_weights()
+        kernels._check_inputs(cfg, corr_pos, src, tgt)
+        N = src.shape[1]
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        cache = self.__dict__.setdefault("_one_cache", {})
+        ent = cache.get((dev, sh, N, id(cfg)))
+        if ent is None:
+            ws = self._workspace(cfg, 1, N, dev)
+            if ws is None:
+                return None
+            pins = self.__dict__.setdefault("_pinned", {})
+            pinned = pins.get((dev, sh))
+            if pinned is None:
+                pinned = pins[(dev, sh)] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            if len(cache) > 256:
+                cache.clear()
+            L = _lib.load()
+            ent = cache[(dev, sh, N, id(cfg))] = (
+                L.pdsc_forward_testing, ctypes.byref(cfg), L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), 1, N),
+                self.__dict__["_ws_cache"], (dev, sh), pinned, pinned.numpy(), ctypes.c_void_p(sh), _hip())
+        fwd, cfgp, nb, wsc, wkey, pinned, pinned_np, sp, hip = ent
+        ws = wsc.get(wkey)
+        if ws is None or ws.numel() < nb:  # another model size / N grew the stream's workspace meanwhile
+            ws = self._workspace(cfg, 1, N, dev)
+        trans = torch.empty((1, 4, 4), dtype=torch.float32, device=dev)
+        labels = torch.empty((1, N), dtype=torch.float32, device=dev)
+        wp = ws.data_ptr()
+        _lib.check(fwd(cfgp, pk.data_ptr(), corr_pos.data_ptr(), src.data_ptr(), tgt.data_ptr(), 1, N,
+                       trans.data_ptr(), labels.data_ptr(), None, None, wp, nb, sp), "pdsc_forward_testing")
+        # the range flag: the forward workspace's first int32 (include/pdsc.h, pdsc_range_status)
+        if hip.hipMemcpyAsync(pinned_np.ctypes.data, ctypes.c_void_p(wp), 4, 2, sp) != 0 \
+                or hip.hipStreamSynchronize(sp) != 0:
+            return None  # the general path reports it through pdsc_range_status
+        if pinned_np[0] != 0:  # marked by the range guard: the general path re-runs it in exact fp32
+            return None
+        return {"final_trans": trans, "final_labels": labels, "M": None}
+
     # --------------------------------------------------------------- forward
     def forward(self, data):
         """models/PointDSC.py:128-197.  Testing mode: bs must be 1 as in :210/:414.
@@ -279,6 +384,10 @@ class PointDSC(nn.Module):
                 cfg, pk, *_rows((corr_pos, src, tgt), i)))
             return {"final_trans": trans, "final_labels": conf, "M": M}
         assert corr_pos.shape[0] == 1  # pick_seeds / post_refinement support bs = 1 only
+        if isinstance(src, torch.Tensor) and src.is_cuda:
+            res = self._forward_one(corr_pos, src, tgt)
+            if res is not None:
+                return res
         trans, labels = self._range_guarded(lambda cfg, pk, i: kernels.forward_testing(
             cfg, pk, *_rows((corr_pos, src, tgt), i),
             ws=self._workspace(cfg, 1, src.shape[1], src.device) if src.is_cuda and i is None else None))

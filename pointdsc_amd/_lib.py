@@ -75,6 +75,7 @@ _PROTOS = {
     "pdsc_encoder_plan": (c_int32, [c_int32, c_int32, c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_attention_timing": (c_int32, [ctypes.POINTER(vp), ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
     "pdsc_forward_timing": (c_int32, [ctypes.POINTER(vp), c_int32, ctypes.POINTER(c_int32)]),
+    "pdsc_diag_qkv_delay": (c_int32, [c_int32]),
     "pdsc_pick_seeds": (c_int32, [vp, vp, c_int32, c_int32, c_float, c_int32, vp, vp, vp]),
     "pdsc_seed_knn_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
     "pdsc_seed_knn": (c_int32, [vp, vp, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, vp, vp, c_size_t,

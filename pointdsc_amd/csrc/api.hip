@@ -14,6 +14,10 @@
 
 using namespace pdsc;
 
+namespace pdsc {
+thread_local int g_diag_qkv_delay = 0;  // pdsc_diag_qkv_delay (tests only)
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -347,18 +351,40 @@ static int run_encoder_fwd(const PackLayout &lay, const float *packed, const flo
                            float *conf, hipStream_t s, Ragged rg, SideStream *ss, const int *bounds, int P) {
     if (!ss) return run_encoder(lay, packed, corr_pos, M, m_layout, d, e, nullptr, normed, normed_s, conf, s, rg);
     std::lock_guard<std::mutex> lock(ss->mu);
+    // The side streams are shared by every caller stream of the device.  A side
+    // stream forked into another thread's graph capture stays in that capture
+    // until it ends: enqueueing there from a stream outside that capture would
+    // record into (or invalidate) the other graph, so such a call runs on one
+    // stream (bitwise the same results).
+    {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone, c2 = hipStreamCaptureStatusNone;
+        unsigned long long id = 0, id2 = 0;
+        HIPCHK(hipStreamGetCaptureInfo(s, &cs, &id));
+        for (int i = 1; i < P; ++i) {
+            HIPCHK(hipStreamGetCaptureInfo(ss->s2[i - 1], &c2, &id2));
+            if (c2 != hipStreamCaptureStatusNone && (cs != hipStreamCaptureStatusActive || id2 != id))
+                return run_encoder(lay, packed, corr_pos, M, m_layout, d, e, nullptr, normed, normed_s, conf, s, rg);
+        }
+    }
     HIPCHK(hipEventRecord(ss->fork, s));
-    for (int i = 1; i < P; ++i) HIPCHK(hipStreamWaitEvent(ss->s2[i - 1], ss->fork, 0));
-    for (int i = 0; i < P; ++i) {
-        const int r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf,
-                                       i ? ss->s2[i - 1] : s, rg, bounds[i], bounds[i + 1] - bounds[i]);
-        if (r != PDSC_OK) return r;
+    int forked = 1, r = PDSC_OK;
+    for (; forked < P; ++forked)
+        if (hipStreamWaitEvent(ss->s2[forked - 1], ss->fork, 0) != hipSuccess) {
+            r = fail(PDSC_ERR_HIP, "hipStreamWaitEvent (fork)");
+            break;
+        }
+    for (int i = 0; r == PDSC_OK && i < P; ++i)
+        r = run_encoder_part(lay, packed, corr_pos, M, m_layout, d, e, normed, normed_s, conf,
+                             i ? ss->s2[i - 1] : s, rg, bounds[i], bounds[i + 1] - bounds[i]);
+    // join every side stream that was forked, on success AND on error: the
+    // caller's stream must not run ahead of work a side stream may still do in
+    // the workspace, and a capture must not end with an unjoined fork
+    for (int i = 1; i < forked; ++i) {
+        const hipError_t a = hipEventRecord(ss->join[i - 1], ss->s2[i - 1]);
+        const hipError_t b = a == hipSuccess ? hipStreamWaitEvent(s, ss->join[i - 1], 0) : a;
+        if (b != hipSuccess && r == PDSC_OK) r = fail(PDSC_ERR_HIP, "join: %s", hipGetErrorString(b));
     }
-    for (int i = 1; i < P; ++i) {
-        HIPCHK(hipEventRecord(ss->join[i - 1], ss->s2[i - 1]));
-        HIPCHK(hipStreamWaitEvent(s, ss->join[i - 1], 0));
-    }
-    return PDSC_OK;
+    return r;
 }
 
 struct NsmBufs {
@@ -651,6 +677,12 @@ int32_t pdsc_attention_timing(void *const *start_events, void *const *stop_event
     return PDSC_OK;
 }
 
+int32_t pdsc_diag_qkv_delay(int32_t loops) {
+    if (loops < 0) return fail(PDSC_ERR_ARG, "loops=%d", loops);
+    g_diag_qkv_delay = loops;
+    return PDSC_OK;
+}
+
 int32_t pdsc_forward_timing(void *const *events, int32_t capacity, int32_t *count) {
     if (capacity > 0 && (!events || !count)) return fail(PDSC_ERR_ARG, "null events/count with capacity %d", capacity);
     g_fev = reinterpret_cast<hipEvent_t *>(const_cast<void **>(events));
@@ -850,6 +882,7 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
         HIPCHK(launch_ragged_setup(counts, B, cfg->ratio, f.nv, f.sv, s));
         rg.nv = f.nv;
         rg.sv = f.sv;
+        rg.eq = std::all_of(counts, counts + B, [N](int32_t n) { return n == N; });
         if (ragged_order_on()) {  // each part's attention launches order that part's pairs
             for (int i = 0; i < parts; ++i)
                 HIPCHK(launch_ragged_order(counts + bounds[i], bounds[i + 1] - bounds[i], f.po + bounds[i], s));

@@ -210,7 +210,7 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
         AttnGridH3 g = w64_grid(B, N);
         if (g.Npad != Npad || nsplit != w64_nsplit(B, N)) return hipErrorInvalidValue;
         g.nsplit = nsplit;  // slots past the split grid's own: empty splits (st0 >= st1)
-        const int nwg = rg.nv ? 0 : w64_sk_wgs(B, N);
+        const int nwg = rg.nv && !rg.eq ? 0 : w64_sk_wgs(B, N);
         if (nwg) {
             hipLaunchKernelGGL((attention_w64_sk_kernel<true>), dim3(nwg), dim3(W64_NW * 64), W64_LDS, s,
                                static_cast<const _Float16 *>(q), static_cast<const _Float16 *>(k),
@@ -1907,8 +1907,7 @@ hipError_t launch_pw_first(const float *packed, const PackLayout &lay, const flo
 hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, bool f32, const float *opart,
                          const float *ml, int nsplit, int B, int N, int Npad, const float *feat_in, float *feat,
                          void *q, void *k, void *v, float *vexp, hipStream_t s) {
-    const char *dd = getenv("PDSC_DIAG_QKV_DELAY");  // tests only: delay the split's K / V workgroups
-    const int delay = dd ? atoi(dd) : 0;
+    const int delay = g_diag_qkv_delay;  // tests only (pdsc_diag_qkv_delay): delay the split's K / V workgroups
     _Float16 *Q = static_cast<_Float16 *>(q), *K = static_cast<_Float16 *>(k), *V = static_cast<_Float16 *>(v);
     if (use_pw2(B, Npad, f32)) {
         const W2Sched S = sched_qkv(sched_msg(msg3(lay.layer[layer])), dense4(lay.layer[layer + 1]));

@@ -136,10 +136,15 @@ inline PackLayout make_layout(int L, int in_dim) {
 // Every pair's buffers keep the batch stride N (the largest pair); pair b uses
 // its first nv[b] rows and has sv[b] = int(nv[b] * ratio) seeds (S = the
 // largest).  nv == sv == nullptr: a uniform batch (every pair N rows, S seeds).
+extern thread_local int g_diag_qkv_delay;  // api.hip: pdsc_diag_qkv_delay (tests only)
 struct Ragged {
     const int *nv = nullptr, *sv = nullptr;
     // the attention's pair order (longest pairs first, dealt over the XCDs), or null
     const int *po = nullptr;
+    // every count equals the padded N (host-known): the attention takes the
+    // uniform batch's form (stream-K on the w64 plan), so such a call is bitwise
+    // the uniform entry's (same key partition, same fp32 combine order)
+    bool eq = false;
     PDSC_DEV int n(int b, int N) const { return nv ? nv[b] : N; }
     PDSC_DEV int s(int b, int S) const { return sv ? sv[b] : S; }
 };

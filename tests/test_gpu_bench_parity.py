@@ -133,3 +133,55 @@ def test_bench_pairs_raw_weights(precision, gpu_device):
         sc = (conf * O.local_max(ps[i]["src_keypts"], conf, p["nms_radius"])).astype(np.float32)
         assert np.array_equal(st["seeds"][i], np.argsort(-sc, kind="stable")[:st["seeds"].shape[1]]), i
         _pinned_downstream(int(i), st, ps, sd, p)
+
+
+def test_b65_both_attention_plans_vs_reference(gpu_device, capsys):
+    """The first 65 bench pairs: 65 x 1000 leaves the fused plan for the
+    64-query-wave split plan (pdsc_encoder_plan 2, two key splits per query
+    block), where the uniform entry runs the stream-K attention and a ragged
+    call with unequal padding runs the split grid -- two key partitions, two
+    fp32 combine orders, so a pair's bits depend on the plan (round 5 measured
+    poses 2.1e-4 apart, profiles/r05_ragged_halves_eq.log).  EACH plan is held
+    to the reference's own outputs (tests/golden/bench_3dmatch_1k_tf.npz) by the
+    rules above: labels bit-exact on all 65 pairs, poses within 1e-4 or the
+    near-tie explanation (logits within the fp32 envelope, seeds / kNN rows
+    different only by near-ties, the oracle on our seeds and kNN rows within
+    1e-4).  The distances of both plans are printed for the record."""
+    import ctypes
+    from pointdsc_amd import _lib, kernels
+    from pointdsc_amd.PointDSC import PointDSC
+    from pointdsc_amd.synthetic import BENCH_CLS, PRESETS, synthetic_pair, trained_state_dict
+    g = load_golden("bench_3dmatch_1k_tf")
+    P, N = 65, int(g["num_corr"])
+    plan = ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(P, N, 0, ctypes.byref(plan)), "encoder_plan")
+    assert plan.value == 2
+    p = PRESETS[str(g["preset"])]
+    m = PointDSC(in_dim=6, num_layers=12, num_channels=128, num_iterations=10, ratio=0.1,
+                 inlier_threshold=p["inlier_threshold"], sigma_d=p["sigma_d"], k=40, nms_radius=p["nms_radius"])
+    sd = trained_state_dict(str(g["preset"]), 12, *BENCH_CLS)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(gpu_device).eval()
+    ps = [synthetic_pair(N, int(g["pair_seed_base"]) + i, str(g["preset"])) for i in range(P)]
+    data = {k: torch.from_numpy(np.stack([q[k] for q in ps])).to(gpu_device)
+            for k in ("corr_pos", "src_keypts", "tgt_keypts")}
+    cfg, pk = m.pdsc_config(), m.packed_weights()
+    with torch.no_grad():
+        uni = kernels.forward_stages(cfg, pk, data["corr_pos"], data["src_keypts"], data["tgt_keypts"])
+        # the split grid: a ragged call padded to N + 1 rows (counts all N, not the padded N)
+        pad = {k: torch.cat([v, torch.zeros_like(v[:, :1])], 1) for k, v in data.items()}
+        T2, L2, st2 = kernels.forward_ragged(cfg, pk, pad["corr_pos"], pad["src_keypts"], pad["tgt_keypts"], [N] * P,
+                                             debug=True)
+    st2 = dict(st2, final_trans=T2, final_labels=L2[:, :N], conf=st2["conf"][:, :N])
+    report = {}
+    for name, st in (("stream-K (uniform entry)", uni), ("split grid (ragged entry)", st2)):
+        st = {k: v.cpu().numpy() for k, v in st.items()}
+        assert np.array_equal(st["final_labels"].astype(np.uint8), g["final_labels"][:P]), name
+        d = np.abs(st["final_trans"] - g["final_trans"][:P]).reshape(P, -1).max(1)
+        far = np.nonzero(d > POSE_ATOL)[0]
+        for i in far:
+            _explain(int(i), g, st, ps, sd, p, gpu_device)
+        report[name] = {"max_pose_diff": float(d.max()), "pairs_past_1e-4": far.tolist()}
+    dd = float((uni["final_trans"] - T2).abs().max())
+    with capsys.disabled():
+        print(f"\n[b65] vs reference: {report}; stream-K vs split grid max pose diff {dd:.3g}")

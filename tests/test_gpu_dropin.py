@@ -107,3 +107,43 @@ def test_state_dict_after_forward_matches_reference_layout(gpu_device):
     for k, v in before.items():
         assert after[k].shape == v.shape and torch.equal(after[k].cpu(), v), k
     assert all(p.is_leaf for p in m.parameters())
+
+
+def test_forward_under_inference_mode_then_edit(gpu_device):
+    """the first forward inside torch.inference_mode() must
+    work, and leave ordinary tensors: an in-place edit, an optimizer step and
+    load_state_dict outside it afterwards work and show in the next forward."""
+    m, data = _model(gpu_device), _data(gpu_device)
+    opt = torch.optim.SGD([m.sigma_spat], lr=0.0)
+    s0 = m.sigma_spat.detach().clone()
+    with torch.inference_mode():
+        r0 = m(data)
+    assert not m.sigma_spat.is_inference()
+    with torch.no_grad():
+        m.sigma_spat.mul_(1.5)
+    r1 = m(data)
+    assert not _same(r0, r1) and _same(r1, _fresh(gpu_device, m, data))
+    # the optimizer's reference (taken before the first forward) is the model's tensor
+    assert opt.param_groups[0]["params"][0] is m.sigma_spat
+    with torch.no_grad():
+        opt.param_groups[0]["params"][0].copy_(s0)
+    with torch.inference_mode():
+        r2 = m(data)
+    assert _same(r2, r0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    assert _same(m(data), r0)
+
+
+def test_unrelated_registration_keeps_packing(gpu_device):
+    """building another module (a process-wide
+    registration) does not re-pack this model; replacing one of its own
+    parameters does."""
+    m, data = _model(gpu_device), _data(gpu_device)
+    r0 = m(data)
+    pc = m.pack_count
+    nn.Linear(4, 4)
+    assert _same(m(data), r0) and m.pack_count == pc
+    m.encoder.layer0.bias = nn.Parameter(m.encoder.layer0.bias.detach().clone() + 0.25)
+    r1 = m(data)
+    assert m.pack_count == pc + 1 and _same(r1, _fresh(gpu_device, m, data))

@@ -443,14 +443,17 @@ def test_pw_qkv_split_delayed_readers(gpu_device, monkeypatch):
     """The split pw_mid's K and V workgroups read the layer's residual rows that
     the Q workgroup replaces with the new PointCN rows: the rows ping-pong
     between two feat buffers, so delaying the K / V workgroups until the Q one
-    has stored (PDSC_DIAG_QKV_DELAY: s_sleep loops before their first load) must
+    has stored (pdsc_diag_qkv_delay: s_sleep loops before their first load) must
     leave every output bit unchanged.  Before the ping-pong this read the new
     rows as the residual (wrong K / V)."""
     for B, N in ((1, 1000), (2, 777)):
         ref = _fusion_outputs(gpu_device, B, N)
-        monkeypatch.setenv("PDSC_DIAG_QKV_DELAY", "24")  # ~100 us: longer than the whole pw_mid launch
-        late = _fusion_outputs(gpu_device, B, N)
-        monkeypatch.delenv("PDSC_DIAG_QKV_DELAY")
+        from pointdsc_amd import _lib
+        _lib.check(_lib.load().pdsc_diag_qkv_delay(24), "pdsc_diag_qkv_delay")  # ~100 us: longer than pw_mid
+        try:
+            late = _fusion_outputs(gpu_device, B, N)
+        finally:
+            _lib.load().pdsc_diag_qkv_delay(0)
         for k, v in ref.items():
             assert np.array_equal(v, late[k]), (B, N, k)
 

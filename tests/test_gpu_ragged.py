@@ -10,12 +10,17 @@ evaluation/test_3DMatch.py:33-53 feeds them one by one at bs = 1).  Run with -m 
   * no cross-pair leakage: a pair's outputs are bitwise those of the same pair in
     a batch of the same shape (B, N: the same kernel plan) made of copies of it;
   * against per-pair ``forward`` calls (other launch plans, other fp32 summation
-    orders): labels bitwise, poses within 2e-4 (as test_batched_equals_single)."""
+    orders): labels bitwise, poses within north_star's 1e-4 -- or, where the two
+    fp32 orders decided a seed / kNN near-tie differently, BOTH results held to
+    the oracle by the near-tie rules (conftest.assert_held_to_oracle);
+  * counts all equal to the padded N: bitwise the uniform entry (the same
+    attention form, Ragged::eq), at every plan (fused 64 / 128 pairs, the
+    64-query-wave stream-K plan at 65)."""
 import numpy as np
 import pytest
 import torch
 
-from conftest import assert_knn_equivalent
+from conftest import assert_held_to_oracle, assert_knn_equivalent
 
 pytestmark = pytest.mark.gpu
 
@@ -41,6 +46,35 @@ def _pairs(sizes, seed=77):
 
 def _datas(ps, dev):
     return [{k: torch.from_numpy(q[k])[None].to(dev) for k in ("corr_pos", "src_keypts", "tgt_keypts")} for q in ps]
+
+
+def _ragged_stages(m, ds):
+    """forward_list's call with every stage's output: (T, L, stage dict on host, counts)."""
+    from pointdsc_amd import kernels
+    corr, counts = kernels.pad_pairs([d["corr_pos"] for d in ds])
+    src, _ = kernels.pad_pairs([d["src_keypts"] for d in ds])
+    tgt, _ = kernels.pad_pairs([d["tgt_keypts"] for d in ds])
+    T, L, st = kernels.forward_ragged(m.pdsc_config(), m.packed_weights(), corr, src, tgt, counts, debug=True)
+    return T, L, {k: v.cpu().numpy() for k, v in st.items()}, counts
+
+
+def _vs_single(m, sd, q, d, Tb, Lb, stb, n, what):
+    """Pair b of a batched call against its own bs = 1 forward: labels bitwise;
+    poses within 1e-4, or both held to the oracle by the near-tie rules."""
+    from pointdsc_amd import kernels
+    r = m(dict(d, testing=True))
+    assert torch.equal(r["final_labels"][0], Lb[:n]), what
+    dT = float((r["final_trans"][0] - Tb).abs().max())
+    if dT <= 1e-4:
+        return "equal"
+    one = kernels.forward_stages(m.pdsc_config(), m.packed_weights(), d["corr_pos"], d["src_keypts"], d["tgt_keypts"])
+    one = {k: v[0].cpu().numpy() for k, v in one.items()}
+    S = int(n * 0.1)
+    for name, (lab, tr, conf, seeds, knn) in {
+            "single": (one["final_labels"], one["final_trans"], one["conf"], one["seeds"], one["knn"]),
+            "batched": (Lb[:n].cpu().numpy(), Tb.cpu().numpy(), stb["conf"][:n], stb["seeds"][:S], stb["knn"][:S])}.items():
+        assert_held_to_oracle(q, lab, tr, conf, seeds, knn, sd, f"{what} {name} (dT {dT:.3g})", num_layers=12)
+    return "near-tie"
 
 
 @pytest.mark.parametrize("precision", ["h3", "f32"])
@@ -110,15 +144,24 @@ def test_ragged_uniform_equals_batched(gpu_device):
     assert torch.equal(T, T2) and torch.equal(L, L2)
 
 
-@pytest.mark.parametrize("B", [64, 128])
+@pytest.mark.parametrize("B", [64, 65, 128])
 def test_ragged_halves_equal_uniform(B, gpu_device):
     """From 32 pairs on the fused plan a ragged batch runs the encoder as two half
     batches on two streams (api.hip: run_encoder_fwd), each keeping the whole
     batch's plan (at 64 pairs a half of 32 alone would take the unfused chains);
     with every count N it is bitwise the uniform forward, which stays on one
     stream.  (Odd splits: test_ragged_vs_single_forwards[130] and the other
-    ragged tests, which all run with the halves.)"""
-    from pointdsc_amd import kernels
+    ragged tests, which all run with the halves.)  65 pairs leave the fused plan
+    for the 64-query-wave split plan (pdsc_encoder_plan 2, two key splits), where
+    the uniform entry runs the stream-K attention: a ragged call whose counts
+    all equal N takes it too (Ragged::eq), so it is bitwise the uniform call --
+    round 5 measured conf 8.6e-5 / poses 2.1e-4 apart when the ragged call ran
+    the split grid, another key partition (profiles/r05_ragged_halves_eq.log)."""
+    import ctypes
+    from pointdsc_amd import _lib, kernels
+    plan = ctypes.c_int32()
+    _lib.check(_lib.load().pdsc_encoder_plan(B, 1000, 0, ctypes.byref(plan)), "encoder_plan")
+    assert plan.value == (2 if B == 65 else 1), (B, plan.value)
     from pointdsc_amd.synthetic import synthetic_batch
     m, _ = _model(gpu_device)
     d = synthetic_batch(B, 1000, seed=83)
@@ -155,15 +198,17 @@ def test_ragged_halves_graph_capture(gpu_device):
 def test_ragged_vs_single_forwards(B, gpu_device):
     """forward_list over B pairs of N in [600, 1400] (B = 130: the fused
     attention + pointwise launches) against B separate ``forward`` calls."""
-    m, _ = _model(gpu_device)
+    m, sd = _model(gpu_device)
     rng = np.random.RandomState(B)
     sizes = rng.randint(600, 1401, size=B).tolist()
-    ds = _datas(_pairs(sizes, seed=80 + B), gpu_device)
+    ps = _pairs(sizes, seed=80 + B)
+    ds = _datas(ps, gpu_device)
     res = m.forward_list(ds)
+    T, L, st, counts = _ragged_stages(m, ds)
     for b in range(0, B, max(1, B // 16)):
-        r = m(dict(ds[b], testing=True))
-        assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
-        np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
+        assert torch.equal(T[b], res[b]["final_trans"][0])
+        stb = {k: v[b] for k, v in st.items()}
+        _vs_single(m, sd, ps[b], ds[b], T[b], L[b], stb, counts[b], f"pair {b} (N={counts[b]})")
 
 
 @pytest.mark.parametrize("sizes", [[777, 1000, 3000, 2111, 5000],  # key-split plan
@@ -196,17 +241,23 @@ def test_forward_list_small_pairs(gpu_device):
     """Pairs with count <= k (their forward clips k to count - 1, :250) in a list
     with larger ones: forward_list runs them alone (bitwise their own forward),
     the rest as one ragged batch; every pair matches its own forward."""
-    m, _ = _model(gpu_device)
+    m, sd = _model(gpu_device)
     sizes = [30, 1000, 41, 800, 12]
-    ds = _datas(_pairs(sizes, seed=82), gpu_device)
+    ps = _pairs(sizes, seed=82)
+    ds = _datas(ps, gpu_device)
     res = m.forward_list(ds)
+    big = [b for b, n in enumerate(sizes) if n > 40]
+    T, L, st, _ = _ragged_stages(m, [ds[b] for b in big])
     for b, n in enumerate(sizes):
         r = m(dict(ds[b], testing=True))
         assert res[b]["final_labels"].shape == (1, n)
         assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
         if n <= 40:
             assert torch.equal(r["final_trans"], res[b]["final_trans"]), b
-        np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
+            continue
+        j = big.index(b)
+        assert torch.equal(T[j], res[b]["final_trans"][0])
+        _vs_single(m, sd, ps[b], ds[b], T[j], L[j], {k: v[j] for k, v in st.items()}, n, f"pair {b} (N={n})")
 
 
 def test_ragged_w64_extra_split_slots(gpu_device):
@@ -214,18 +265,20 @@ def test_ragged_w64_extra_split_slots(gpu_device):
     slots per query block (the stream-K count a uniform batch of this shape
     would use); a ragged batch runs the split grid, whose one key split leaves
     slots 1 and 2 as empty splits (m = -inf, skipped by the combine).  Against
-    per-pair ``forward`` calls: labels bitwise, poses within 2e-4."""
+    per-pair ``forward`` calls: labels bitwise, poses within 1e-4 or both held
+    to the oracle (near-tie rules)."""
     import ctypes
     from pointdsc_amd import _lib
-    m, _ = _model(gpu_device)
+    m, sd = _model(gpu_device)
     sizes = [1500 - 17 * i for i in range(24)]
     plan, npad, ns = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
     _lib.check(_lib.load().pdsc_encoder_plan(24, 1500, 0, ctypes.byref(plan)), "encoder_plan")
     _lib.check(_lib.load().pdsc_attention_layout(24, 1500, 0, ctypes.byref(npad), ctypes.byref(ns)), "layout")
     assert plan.value == 2 and ns.value == 3, (plan.value, ns.value)
-    ds = _datas(_pairs(sizes, seed=91), gpu_device)
+    ps = _pairs(sizes, seed=91)
+    ds = _datas(ps, gpu_device)
     res = m.forward_list(ds)
+    T, L, st, counts = _ragged_stages(m, ds)
     for b in range(0, 24, 3):
-        r = m(dict(ds[b], testing=True))
-        assert torch.equal(r["final_labels"], res[b]["final_labels"]), b
-        np.testing.assert_allclose(r["final_trans"].cpu().numpy(), res[b]["final_trans"].cpu().numpy(), atol=2e-4)
+        assert torch.equal(T[b], res[b]["final_trans"][0])
+        _vs_single(m, sd, ps[b], ds[b], T[b], L[b], {k: v[b] for k, v in st.items()}, counts[b], f"pair {b}")

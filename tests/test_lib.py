@@ -159,3 +159,46 @@ def test_flat_weight_views_track_edits():
     e = mod._REGISTRATION_EPOCH[0]
     m.classification[4].bias = nn.Parameter(torch.zeros(1))
     assert mod._REGISTRATION_EPOCH[0] != e
+
+
+def test_flatten_keeps_parameter_objects_and_inference_mode():
+    """the flat buffer keeps every Parameter / buffer OBJECT (an
+    optimizer built before the first forward still updates the model, and its
+    steps bump the flat version), it is built outside inference mode (a first
+    forward under torch.inference_mode() leaves ordinary tensors: later in-place
+    edits and load_state_dict outside it work), and a registration in another
+    module does not count as a change of this model's tensors."""
+    import torch
+    import torch.nn as nn
+    from pointdsc_amd import PointDSC as mod
+    m = mod.PointDSC(num_layers=2)
+    ids = {k: id(v) for k, v in m.named_parameters()}
+    bufs = {k: id(v) for k, v in m.named_buffers()}
+    opt = torch.optim.SGD(m.parameters(), lr=0.5)
+    w0 = m.encoder.layer0.weight
+    w0.grad = torch.ones_like(w0)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    cfg = m.pdsc_config()
+    with torch.inference_mode():
+        flat = m._flatten(m._packable(cfg), device_only=False)
+        _ = flat._version  # readable: not an inference tensor
+    assert flat is not None and not flat.is_inference()
+    assert {k: id(v) for k, v in m.named_parameters()} == ids
+    assert {k: id(v) for k, v in m.named_buffers()} == bufs
+    assert m.encoder.layer0.weight is w0 and torch.equal(w0.grad, torch.ones_like(w0))
+    assert all(not v.is_inference() for v in m.state_dict().values())
+    assert all(torch.equal(m.state_dict()[k], before[k]) for k in before)
+    assert flat.data_ptr() <= w0.data_ptr() < flat.data_ptr() + flat.numel() * 4
+    v = flat._version
+    opt.step()  # the optimizer's own Parameter references
+    assert flat._version != v
+    assert torch.allclose(m.encoder.layer0.weight, before["encoder.layer0.weight"] - 0.5)
+    v = flat._version
+    m.load_state_dict(before)  # outside inference mode, after the flatten
+    assert flat._version != v and torch.equal(m.encoder.layer0.weight, before["encoder.layer0.weight"])
+    # identity check after an unrelated registration (what packed_weights does on an epoch bump)
+    st = {"flat": flat, "tensors": m._packable(cfg)}
+    nn.Linear(2, 2)
+    assert m._same_tensors(st, cfg)
+    m.encoder.layer0.bias = nn.Parameter(torch.zeros_like(m.encoder.layer0.bias))
+    assert not m._same_tensors(st, cfg)
