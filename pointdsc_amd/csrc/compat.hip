@@ -12,6 +12,7 @@
 // ops), so computing each pair once halves the VALU work that would otherwise
 // sit right at the write roofline.  Stores are 16 B per lane.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "pdsc_internal.hpp"
@@ -30,7 +31,7 @@ constexpr int CT = 64;  // tile edge (dense kernel)
 // (group-major: out[g][4 lane + e], so each lane's 16-B read is conflict-free).
 template <int E> struct CompatScratch {
     float qx[64 * E], qt[64 * E], out[64 * E];
-    unsigned short qs[64 * E];
+    unsigned qs[64 * E];  // 32-bit: the same byte offset as qx / qt (no separate address)
 };
 
 // M for E (row, column) pairs of this lane, given their squared distances.
@@ -46,7 +47,6 @@ template <int E> struct CompatScratch {
 template <int E>
 PDSC_DEV void compat_n(const float (&xs)[E], const float (&xt)[E], float s2, float rs2, bool s2ok, float kzero,
                        float gmax, CompatScratch<E> &sc, int lane, float (&out)[E]) {
-    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int g = 0; g < E / 4; ++g)
         *reinterpret_cast<f32x4 *>(&sc.out[256 * g + 4 * lane]) = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -54,13 +54,19 @@ PDSC_DEV void compat_n(const float (&xs)[E], const float (&xt)[E], float s2, flo
 #pragma unroll
     for (int q = 0; q < E; ++q) {
         const float dxt = xs[q] - xt[q], sum = xs[q] + xt[q];
-        const bool zero = (dxt * dxt > kzero * sum) && (sum <= gmax);  // NaN, xs = xt = 0 -> exact path
-        const unsigned long long m = __ballot(!zero);
-        if (!zero) {
-            const int pos = cnt + __popcll(m & below);
+        // zero = (dxt^2 > kzero sum) && (sum <= gmax); NaN, xs = xt = 0 -> exact path.
+        // The queue mask as the OR of the two compares' own lane masks (a ballot
+        // of the combined bool widens it to a VGPR and compares it again: 2 VALU
+        // per element), the lane's rank among the queued lanes by v_mbcnt (2 VALU,
+        // instead of and + bcnt x 2)
+        const bool nz0 = !(dxt * dxt > kzero * sum), nz1 = !(sum <= gmax);
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(nz0) | __builtin_amdgcn_ballot_w64(nz1);
+        if (nz0 || nz1) {
+            const int pos = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             sc.qx[pos] = xs[q];
             sc.qt[pos] = xt[q];
-            sc.qs[pos] = (unsigned short)(256 * (q >> 2) + 4 * lane + (q & 3));
+            sc.qs[pos] = (unsigned)(256 * (q >> 2) + 4 * lane + (q & 3));
         }
         cnt += __popcll(m);
     }
@@ -247,43 +253,53 @@ __global__ __launch_bounds__(256) void compat_packed_kernel(const float *__restr
             cs[q][k] = pts[2][cq * 4 + q][k];
             ct[q][k] = pts[3][cq * 4 + q][k];
         }
+    // EDGE: a diagonal block or one that reaches past N (per-element masking);
+    // every other block (all but ~2 / ntile of them) runs without the masks
+    auto rows = [&](auto edge_tag) {
+        constexpr bool EDGE = decltype(edge_tag)::value;
 #pragma unroll
-    for (int r0 = 0; r0 < 4; r0 += RP) {
-        // rows rq + 16 rr, rr = r0 .. r0 + RP - 1.  Elements below the diagonal
-        // (diagonal blocks) or past N are not stored: their distances are set to
-        // pass compat_n's zero test, so they never queue for the exact path.
-        bool skip[RP], any = false;
-        float xs[E], xt[E], out[E];
+        for (int r0 = 0; r0 < 4; r0 += RP) {
+            // rows rq + 16 rr, rr = r0 .. r0 + RP - 1.  Elements below the diagonal
+            // (diagonal blocks) or past N are not stored: their distances are set to
+            // pass compat_n's zero test, so they never queue for the exact path.
+            bool skip[RP], any = false;
+            float xs[E], xt[E], out[E];
 #pragma unroll
-        for (int u = 0; u < RP; ++u) {
-            const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
-            skip[u] = tr > tc || tr >= nt32 || tc >= nt32;
-            any |= !skip[u];
-            const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
-            const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
+            for (int u = 0; u < RP; ++u) {
+                const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
+                skip[u] = EDGE && (tr > tc || tr >= nt32 || tc >= nt32);
+                any |= !skip[u];
+                const float six = pts[0][r][0], siy = pts[0][r][1], siz = pts[0][r][2];
+                const float tix = pts[1][r][0], tiy = pts[1][r][1], tiz = pts[1][r][2];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xs[4 * u + q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
-                xt[4 * u + q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
-                if (skip[u] || i0 + r >= N || j0 + cq * 4 + q >= N) {
-                    xs[4 * u + q] = 4.0f * s2;
-                    xt[4 * u + q] = 0.0f;
+                for (int q = 0; q < 4; ++q) {
+                    xs[4 * u + q] = sqdist3(six, siy, siz, cs[q][0], cs[q][1], cs[q][2]);
+                    xt[4 * u + q] = sqdist3(tix, tiy, tiz, ct[q][0], ct[q][1], ct[q][2]);
+                    if (EDGE && (skip[u] || i0 + r >= N || j0 + cq * 4 + q >= N)) {
+                        xs[4 * u + q] = 4.0f * s2;
+                        xt[4 * u + q] = 0.0f;
+                    }
                 }
             }
-        }
-        if (!__any(any)) continue;  // wave-uniform
-        compat_n<E>(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
+            if (EDGE && !__any(any)) continue;  // wave-uniform
+            compat_n<E>(xs, xt, s2, rs2, s2ok, kzero, gmax, scr[wave], lane, out);
 #pragma unroll
-        for (int u = 0; u < RP; ++u) {
-            if (skip[u]) continue;
-            const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
-            float o[4];
+            for (int u = 0; u < RP; ++u) {
+                if (skip[u]) continue;
+                const int r = rq + 16 * (r0 + u), tr = 2 * ti + (r >> 5);
+                float o[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = (i0 + r >= N || j0 + cq * 4 + q >= N) ? 0.0f : out[4 * u + q];
-            float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
-            *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{o[0], o[1], o[2], o[3]};
+                for (int q = 0; q < 4; ++q)
+                    o[q] = (EDGE && (i0 + r >= N || j0 + cq * 4 + q >= N)) ? 0.0f : out[4 * u + q];
+                float *tile = Mb + (size_t)mpack_tile(tr, tc, nt32) * (MPACK_T * MPACK_T);
+                *reinterpret_cast<f32x4 *>(tile + (r & 31) * MPACK_T + ((cq * 4) & 31)) = f32x4{o[0], o[1], o[2], o[3]};
+            }
         }
-    }
+    };
+    if (ti < tj && j0 + CT <= N)  // workgroup-uniform
+        rows(std::false_type{});
+    else
+        rows(std::true_type{});
 }
 
 hipError_t launch_compat_packed(const float *src, const float *tgt, int B, int N, const float *sigma_d,

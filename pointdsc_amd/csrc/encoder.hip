@@ -141,7 +141,28 @@ static int att_target() {
     }();
     return t;
 }
-static AttnGridH3 prod_grid(int B, int N) { return attention_h3_grid<ATT_NW>(B, N, att_target()); }
+// Waves (x 32 queries) per workgroup of the h3 split-K attention: 4, except 2
+// for batches of at most 16 blocks of 128 queries (single pairs up to N = 2048),
+// whose launch is latency-bound: twice the query blocks, each workgroup's K/V
+// stream shared by 2 waves.  Measured (ms per forward, two A/B rounds on one
+// box, profiles/r06_ab_att_nw.log): 1 x 1000 0.4235 -> 0.417, 1 x 2000 0.531 ->
+// 0.504, 1 x 5000 (not covered) equal; 1 wave 0.4185 / 0.515.  A/B knob
+// PDSC_ATT_NW=1|2|4 (measurement only) sets the small-batch count.
+static int att_nw(int B, int N) {
+    static const int v = [] {
+        const char *e = getenv("PDSC_ATT_NW");
+        const int w = e ? atoi(e) : 2;
+        return (w == 1 || w == 2) ? w : ATT_NW;
+    }();
+    return (long)B * ((N + QB - 1) / QB) <= 16 ? v : ATT_NW;
+}
+static AttnGridH3 prod_grid(int B, int N) {
+    switch (att_nw(B, N)) {
+    case 1: return attention_h3_grid<1>(B, N, att_target());
+    case 2: return attention_h3_grid<2>(B, N, att_target());
+    default: return attention_h3_grid<ATT_NW>(B, N, att_target());
+    }
+}
 
 // The attention's workgroup order, reversed on alternate layers (fused and
 // split-K launches; the stream-K form excepted): a launch
@@ -201,6 +222,26 @@ int attention_nsplit(int B, int N, bool f32, bool w64) {
     return f32 ? f32_grid(B, N).nsplit : (w64 ? w64_nsplit(B, N) : prod_grid(B, N).nsplit);
 }
 
+template <int NW>
+static hipError_t launch_attention_h3(const _Float16 *qs, const _Float16 *ks, const _Float16 *vs, const float *vexp,
+                                      const float *M, bool m_packed, const AttnGridH3 &g, float *opart, float *ml,
+                                      hipStream_t s) {
+    const dim3 grid(g.B * g.nqb * g.nsplit), block(NW * 64);
+    const size_t lds = attention_h3_lds_bytes<NW>();
+    if (g.sps >= 3) {  // long splits: the early-issue loop (attention_h3_core's EARLY)
+        if (m_packed)
+            hipLaunchKernelGGL((attention_h3_kernel<NW, true, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g,
+                               opart, ml);
+        else
+            hipLaunchKernelGGL((attention_h3_kernel<NW, true, false, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g,
+                               opart, ml);
+    } else if (m_packed)
+        hipLaunchKernelGGL((attention_h3_kernel<NW, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart, ml);
+    else
+        hipLaunchKernelGGL((attention_h3_kernel<NW, true, false>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart, ml);
+    return hipGetLastError();
+}
+
 hipError_t launch_attention(const void *q, const void *k, const void *v, const float *vexp, const float *M,
                             int m_layout, bool w64, bool f32, int B, int N, int Npad, int nsplit, float *opart,
                             float *ml, hipStream_t s, Ragged rg, int layer) {
@@ -243,22 +284,10 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     g.po = rg.po;
     g.rev = rg.po ? 0 : zigzag_rev(layer);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
-    const dim3 grid(g.B * g.nqb * g.nsplit), block(ATT_NW * 64);
-    const size_t lds = attention_h3_lds_bytes<ATT_NW>();
-    if (g.sps >= 3) {  // long splits: the early-issue loop (attention_h3_core's EARLY)
-        if (m_packed)
-            hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g,
-                               opart, ml);
-        else
-            hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false, true>), grid, block, lds, s, qs, ks, vs, vexp, M,
-                               g, opart, ml);
-    } else if (m_packed)
-        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, true>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart,
-                           ml);
-    else
-        hipLaunchKernelGGL((attention_h3_kernel<ATT_NW, true, false>), grid, block, lds, s, qs, ks, vs, vexp, M, g, opart,
-                           ml);
-    return hipGetLastError();
+    const int nw = att_nw(B, N);
+    if (nw == 1) return launch_attention_h3<1>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
+    if (nw == 2) return launch_attention_h3<2>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
+    return launch_attention_h3<ATT_NW>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
 }
 
 // fp32 rows [B][N][CH] -> [B][Npad][CH] with zero padding rows (the f32 attention's input)

@@ -215,6 +215,23 @@ hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStre
 constexpr int KNN_BINCAP = 64;
 constexpr int KNN_FASTCAP = 128;
 
+#ifdef KNN_DIAG
+// Diagnostic build only (-DKNN_DIAG): per launch, how many seed rows took each
+// path: [0] bitonic fast path, [1] readlane ranking, [2] radix fallback,
+// [3] fallback histogram passes, [4] fallback rows resolved through a small bin.
+static __device__ unsigned g_knn_paths[8];
+#define KNN_COUNT(i, v) do { if (lane == 0) atomicAdd(&g_knn_paths[i], (unsigned)(v)); } while (0)
+extern "C" int pdsc_diag_knn_paths(unsigned *host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_knn_paths), sizeof(g_knn_paths), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    static const unsigned zero[8] = {};
+    return reset && hipMemcpyToSymbol(HIP_SYMBOL(g_knn_paths), zero, sizeof(zero), 0, hipMemcpyHostToDevice) != hipSuccess
+               ? -1 : 0;
+}
+#else
+#define KNN_COUNT(i, v) do { } while (0)
+#endif
+
 template <int R>
 __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int Nstr, int Sstr,
                                                          int k, int *__restrict__ knn, Ragged rg, int bitonic) {
@@ -337,6 +354,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 }
             int *out = knn + ((size_t)b * Sstr + s) * k;
             if (lane > 0 && lane < (int)want && lane < (int)c) out[lane - 1] = ii;  // drop position 0 (:68)
+            KNN_COUNT(0, 1);
             return;
         }
         if (c <= KNN_FASTCAP) {
@@ -364,11 +382,13 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             int *out = knn + ((size_t)b * Sstr + s) * k;
             if (e0 < (int)c && r0 > 0 && r0 < want) out[r0 - 1] = i0;  // drop position 0 (:68)
             if (e1 < (int)c && r1 > 0 && r1 < want) out[r1 - 1] = i1;
+            KNN_COUNT(1, 1);
             return;
         }
     }
     // Radix fallback, keys re-read from memory (lane l owns keys l + 64 i, so a
     // ballot over lanes visits keys in index order).
+    KNN_COUNT(2, 1);
     const int NI = (N + 63) / 64;
     auto K = [&](int i) -> uint32_t {
         const int j = lane + 64 * i;
@@ -397,6 +417,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         for (int hi = top; hi >= 0; hi -= 8) {
             const int lo = max(hi - 7, 0);
             const uint32_t dm = (2u << (hi - lo)) - 1u;  // digit = bits [lo, hi]
+            KNN_COUNT(3, 1);
 #pragma unroll
             for (int e = 0; e < 4; ++e) hb[lane + 64 * e] = 0;
             __builtin_amdgcn_wave_barrier();
@@ -480,6 +501,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
         pe += __popcll(em);
     }
     __builtin_amdgcn_wave_barrier();
+    if (small_bin) KNN_COUNT(4, 1);
     if (small_bin) {  // the `need` smallest (key, index) of the bin's bin_cnt keys
         for (int e = lane; e < (int)bin_cnt; e += 64) {
             const uint32_t ku = bkey[wave][e];
@@ -512,7 +534,15 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
 // nsm_seed, kabsch_sums; none has a workgroup barrier): 4, unless that leaves
 // fewer than 2 workgroups per CU (a single N = 5000 pair has 500 seeds = 125
 // four-wave workgroups for 256 CUs), then 1 so the seeds spread over all CUs.
-static int seed_wpb(int B, int S) { return (long)B * ((S + 3) / 4) < 512 ? 1 : 4; }
+static int seed_wpb(int B, int S) {
+    static const int force = [] {  // A/B knob PDSC_SEED_WPB=1|2|4 (measurement only)
+        const char *e = getenv("PDSC_SEED_WPB");
+        const int w = e ? atoi(e) : 0;
+        return (w == 1 || w == 2 || w == 4) ? w : 0;
+    }();
+    if (force) return force;
+    return (long)B * ((S + 3) / 4) < 512 ? 1 : 4;
+}
 
 hipError_t launch_knn_select(const float *dist, int B, int N, int S, int k, int *knn, hipStream_t s,
                              Ragged rg) {

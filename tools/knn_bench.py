@@ -20,7 +20,10 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(5)
     res = {}
-    for B, N in ((128, 1000), (128, 1289), (8, 5000), (8, 5003), (1, 1000)):
+    shapes = ((128, 1000), (128, 1289), (8, 5000), (8, 5003), (1, 1000), (1, 5000))
+    if os.environ.get("AB_SHAPES"):
+        shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["AB_SHAPES"].split(",")]
+    for B, N in shapes:
         S = int(0.1 * N)
         f = torch.randn((B, N, 128), generator=g)
         f = (f / f.norm(dim=-1, keepdim=True)).to(dev)
