@@ -418,6 +418,17 @@ int run_nsm(const float *normed, const _Float16 *normed_s, bool f32, const float
     return PDSC_OK;
 }
 
+// The testing forward's fused tail launches (nsm_finish inside the hypotheses'
+// first launch, select_best + post_refine in one): the same bits, two launches
+// fewer per forward.  A/B knob PDSC_TAIL_FUSED=0 (measurement only).
+static bool tail_fused() {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_TAIL_FUSED");
+        return e && e[0] == '0';
+    }();
+    return !off;
+}
+
 // A/B knob (measurement only): PDSC_RAGGED_ORDER=0 keeps the ragged attention
 // workgroups in pair order.
 static bool ragged_order_on() {
@@ -919,20 +930,38 @@ static int32_t forward_testing_impl(const pdsc_config *cfg, const float *packed,
     RET_IF(run_seed_knn(f.normed, f.normed_s, d.f32, f.seeds, d.B, d.N, d.S, d.k, f.kdist, f.knn, s, rg));
     STAGE(4);
     // a7-a8 (:257-282)
-    // per pair: each pair is its own bs = 1 forward, whose allclose spans its S seeds
-    RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm, f.weights,
-                   nullptr, false, s, rg));
+    // per pair: each pair is its own bs = 1 forward, whose allclose spans its S seeds.
+    // The power iterates here; nsm_finish's step (t*, the normalised weights) runs
+    // inside the hypotheses' first launch below (the same bits, one launch fewer).
+    const bool tail = tail_fused();
+    if (!tail) {
+        RET_IF(run_nsm(f.normed, f.normed_s, d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm,
+                       f.weights, nullptr, false, s, rg));
+    } else if (d.T > 0)
+        HIPCHK(launch_nsm_seed(d.f32 ? static_cast<const void *>(f.normed) : static_cast<const void *>(f.normed_s),
+                               d.f32, src, tgt, f.knn, d.B, d.N, d.S, d.k, d.T, sigma, sigma_d, f.nsm.hist, f.nsm.mask,
+                               s, rg));
     STAGE(5);
-    // a9-a10 (:287-335)
+    // a9-a10 (:280-282, :287-335)
     HIPCHK(launch_hypotheses(src, tgt, f.knn, f.weights, d.B, d.N, d.S, d.k, cfg->inlier_threshold,
-                             f.seed_trans, f.counts, f.hsums, s, rg));
-    HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
-                              nullptr, nullptr, final_trans, final_labels, s, rg, f.conf, f.range));
-    if (dbg->trans_pre_refine)
-        HIPCHK(hipMemcpyAsync(dbg->trans_pre_refine, final_trans, sizeof(float) * 16 * d.B, hipMemcpyDeviceToDevice, s));
-    STAGE(6);
-    // a11 (:186, :403-438)
-    HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s, rg, f.range));
+                             f.seed_trans, f.counts, f.hsums, s, rg, tail ? f.nsm.hist : nullptr, f.nsm.mask, d.T,
+                             f.weights));
+    if (dbg->trans_pre_refine || !tail) {  // the pose before refinement: the two launches
+        HIPCHK(launch_select_best(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
+                                  nullptr, nullptr, final_trans, final_labels, s, rg, f.conf, f.range));
+        if (dbg->trans_pre_refine)
+            HIPCHK(hipMemcpyAsync(dbg->trans_pre_refine, final_trans, sizeof(float) * 16 * d.B, hipMemcpyDeviceToDevice,
+                                  s));
+        STAGE(6);
+        // a11 (:186, :403-438)
+        HIPCHK(launch_post_refine(final_trans, src, tgt, d.B, d.N, cfg->refine_threshold, s, rg, f.range));
+    } else {
+        // a10 best + a11 in one launch (select_best's and post_refine's workgroup
+        // bodies back to back; the stage split of the two is then not measured)
+        STAGE(6);
+        HIPCHK(launch_best_refine(src, tgt, f.seed_trans, f.counts, d.B, d.N, d.S, cfg->inlier_threshold,
+                                  cfg->refine_threshold, final_trans, final_labels, s, rg, f.conf, f.range));
+    }
     STAGE(7);
 #undef STAGE
     if (dbg->conf) HIPCHK(hipMemcpyAsync(dbg->conf, f.conf, sizeof(float) * d.B * d.N, hipMemcpyDeviceToDevice, s));

@@ -214,7 +214,7 @@ PDSC_DEV f32x16 mfma_w3x(f16x8 wh, f16x8 wm, f16x8 wl, f16x8 xh, f16x8 xl, f32x1
 constexpr int ST_PER_WAVE = 256, ST_WGS = 64;  // (192 + 3 c .. : the fused chain's chunk c, w2_layer)
 static __device__ unsigned long long g_att_stamps[ST_WGS * 4 * ST_PER_WAVE];
 PDSC_DEV unsigned long long *att_stamp_ptr(int wave) {
-    return (blockIdx.x % 16 == 0 && blockIdx.x / 16 < ST_WGS && wave < 4)
+    return (blockIdx.x % 16 == 0 && blockIdx.x / 16 < ST_WGS && wave < 4 && blockIdx.z == 0)
                ? g_att_stamps + ((blockIdx.x / 16) * 4 + wave) * ST_PER_WAVE
                : nullptr;
 }

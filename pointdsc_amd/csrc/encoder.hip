@@ -148,15 +148,31 @@ static int att_target() {
 // box, profiles/r06_ab_att_nw.log): 1 x 1000 0.4235 -> 0.417, 1 x 2000 0.531 ->
 // 0.504, 1 x 5000 (not covered) equal; 1 wave 0.4185 / 0.515.  A/B knob
 // PDSC_ATT_NW=1|2|4 (measurement only) sets the small-batch count.
+static bool att_tiny(int B, int N);
 static int att_nw(int B, int N) {
     static const int v = [] {
         const char *e = getenv("PDSC_ATT_NW");
         const int w = e ? atoi(e) : 2;
         return (w == 1 || w == 2) ? w : ATT_NW;
     }();
+    if (att_tiny(B, N)) return 1;
     return (long)B * ((N + QB - 1) / QB) <= 16 ? v : ATT_NW;
 }
+// The smallest batches (at most 8 query blocks of 128: a single pair to N =
+// 1024): one-wave workgroups whose key splits fill ONE round of 256 slots
+// (a 1000-key pair: 32 blocks x 8 splits of 4 tiles) instead of 16 blocks x 16
+// splits of 2 -- half the split partials, so pw_mid combines them itself
+// (use_precombine: fewer than 16 splits) and the combine_rows launch goes.
+// A/B knob PDSC_ATT_TINY=0 (measurement only).
+static bool att_tiny(int B, int N) {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_ATT_TINY");
+        return e && e[0] == '0';
+    }();
+    return !off && (long)B * ((N + QB - 1) / QB) <= 8;
+}
 static AttnGridH3 prod_grid(int B, int N) {
+    if (att_tiny(B, N)) return attention_h3_grid<1>(B, N, std::min(att_target(), 256));
     switch (att_nw(B, N)) {
     case 1: return attention_h3_grid<1>(B, N, att_target());
     case 2: return attention_h3_grid<2>(B, N, att_target());
@@ -841,10 +857,14 @@ PDSC_DEV void pcn_qkv8(const float *Xin, float *Xout, const float *__restrict__ 
         asm volatile("" ::: "memory");
         if (lo) dense_tile_w<CH, CH, EPI_BN_RELU, 1, false>(Xin, S132, pa, pk, d.pcn, 0, w4, Xout, S132, nullptr, lane);
         __syncthreads();  // Xout complete; Xin is dead (it now holds the split copy of Xout)
+        CH_STAMP(155);
         char *Xs = reinterpret_cast<char *>(const_cast<float *>(Xin));
         split_tile<PTT, 512>(Xout, S132, Xs, tid);
         if (only == 0) store_rows<PTT, 512>(Xout, S132, feat, p0, PTT, tid);
         __syncthreads();
+        CH_STAMP(156);
+        CH_STAMP(157);
+        CH_STAMP(158);
         if (only == 0) {
             if (lo) dense_split<SPLIT_Q, 1>(Xs, pb, pk, d.q, w4, Q, p0, lane);
         } else if (only == 1) {
@@ -852,6 +872,7 @@ PDSC_DEV void pcn_qkv8(const float *Xin, float *Xout, const float *__restrict__ 
         } else {
             dense_split<SPLIT_V, 1>(Xs, pb, pk, d.v, w4, V, p0, lane, Xout, vexp, lo);  // Xout is dead
         }
+        CH_STAMP(159);
         return;
     }
     if (lo) {

@@ -921,6 +921,28 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
 }
 
 // w = v_{t*} / (sum v_{t*} + 1e-6)  (models/PointDSC.py:280-282)
+// The first iterate t* (1-based; T when none) at which every one of the nq
+// seeds' allclose bits from q0 on is set: torch.allclose over the iterate the
+// reference compares at once (:354).  Wave-uniform.
+PDSC_DEV int nsm_tstar(const unsigned *__restrict__ seed_flags, size_t q0, size_t nq, int T, int lane) {
+    unsigned all = 0xffffffffu;
+    if (T > 0)
+        for (size_t q = lane; q < nq; q += 64) all &= seed_flags[q0 + q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) all &= (unsigned)__shfl_xor((int)all, o);
+    const unsigned m = all & ((T >= 32) ? 0xffffffffu : ((1u << T) - 1u));
+    return m ? (__ffs(m)) : T;
+}
+// This lane's normalised weight of seed row `row` (= b * S + s) from its
+// iterate t* (lanes >= k: 0).
+PDSC_DEV float nsm_weight(const float *__restrict__ hist, size_t row, int tstar, int k, int T, int lane) {
+    float v = 1.0f;
+    if (tstar > 0 && lane < k) v = hist[(row * T + (tstar - 1)) * k + lane];
+    if (lane >= k) v = 0.0f;
+    const float sum = wave_sum(v);
+    return lane < k ? v / (sum + 1e-6f) : 0.0f;
+}
+
 __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict__ hist,
                                                         const unsigned *__restrict__ seed_flags, int S,
                                                         int k, int T, int batch_global, float *__restrict__ weights,
@@ -933,18 +955,9 @@ __global__ __launch_bounds__(64) void nsm_finish_kernel(const float *__restrict_
     // gridDim.y * S seeds of the call (the training forward's [bs * S, k] iterate)
     // (ragged batches run per pair: pdsc_forward_testing_ragged is B bs = 1 forwards)
     const size_t q0 = batch_global ? 0 : (size_t)b * S, nq = batch_global ? (size_t)gridDim.y * S : (size_t)Sb;
-    unsigned all = 0xffffffffu;
-    if (T > 0)
-        for (size_t q = a; q < nq; q += 64) all &= seed_flags[q0 + q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) all &= (unsigned)__shfl_xor((int)all, o);
-    const unsigned m = all & ((T >= 32) ? 0xffffffffu : ((1u << T) - 1u));
-    const int tstar = m ? (__ffs(m)) : T;  // 1-based iterate index
-    float v = 1.0f;
-    if (tstar > 0 && a < k) v = hist[(((size_t)b * S + s) * T + (tstar - 1)) * k + a];
-    if (a >= k) v = 0.0f;
-    const float sum = wave_sum(v);
-    if (a < k) weights[((size_t)b * S + s) * k + a] = v / (sum + 1e-6f);
+    const int tstar = nsm_tstar(seed_flags, q0, nq, T, a);  // 1-based iterate index
+    const float w = nsm_weight(hist, (size_t)b * S + s, tstar, k, T, a);
+    if (a < k) weights[((size_t)b * S + s) * k + a] = w;
     if (s == 0 && a == 0 && iters_used) iters_used[b] = tstar;
 }
 
@@ -970,21 +983,33 @@ PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[
 // SOLVE (small batches, kabsch_small): lane 0 of the seed's wave also finishes
 // the Kabsch solve (kabsch_finish on the same 15 sums kabsch_solve_kernel would
 // read back: the same bits) and writes trans -- one launch instead of two.
-template <bool SOLVE>
+// FIN (the testing forward): the seed's NSM weights are finished here, as
+// nsm_finish_kernel computes them (nsm_tstar over the pair's seeds, nsm_weight;
+// the same bits), and written to `weights` -- one launch fewer per forward.
+template <bool SOLVE, bool FIN = false>
 __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restrict__ src,
                                                           const float *__restrict__ tgt,
                                                           const int *__restrict__ knn,
                                                           const float *__restrict__ weights, int N,
                                                           int S, int k, float *__restrict__ sums, Ragged rg,
-                                                          float *__restrict__ trans) {
+                                                          float *__restrict__ trans, const float *__restrict__ hist = nullptr,
+                                                          const unsigned *__restrict__ seed_flags = nullptr, int T = 0,
+                                                          float *__restrict__ wout = nullptr) {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
     const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (s >= rg.s(b, S)) return;  // (N, S: the strides; knn entries lie below this pair's count)
+    const int Sb = rg.s(b, S);
+    if (s >= Sb) return;  // (N, S: the strides; knn entries lie below this pair's count)
     const float *sb = src + (size_t)b * N * 3, *tb = tgt + (size_t)b * N * 3;
     float w = 0, ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
+    float wf = 0.0f;
+    if constexpr (FIN) {
+        const int tstar = nsm_tstar(seed_flags, (size_t)b * S, (size_t)Sb, T, lane);
+        wf = nsm_weight(hist, (size_t)b * S + s, tstar, k, T, lane);
+        if (lane < k) wout[((size_t)b * S + s) * k + lane] = wf;
+    }
     if (lane < k) {
         const int j = min(max(knn[((size_t)b * S + s) * k + lane], 0), N - 1);
-        w = weights[((size_t)b * S + s) * k + lane];
+        w = FIN ? wf : weights[((size_t)b * S + s) * k + lane];
         ax = sb[3 * j];
         ay = sb[3 * j + 1];
         az = sb[3 * j + 2];
@@ -1117,15 +1142,26 @@ static bool kabsch_small(int n) {
 
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             float *sums, hipStream_t s, Ragged rg) {
+                             float *sums, hipStream_t s, Ragged rg, const float *hist, const unsigned *seed_flags,
+                             int T, float *wout) {
     const int wpb = seed_wpb(B, S);
     const int n = B * S;
+    const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
+    const bool fin = hist != nullptr;
     if (kabsch_small(n)) {
-        hipLaunchKernelGGL(kabsch_sums_kernel<true>, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn,
-                           weights, N, S, k, sums, rg, seed_trans);
+        if (fin)
+            hipLaunchKernelGGL((kabsch_sums_kernel<true, true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k,
+                               sums, rg, seed_trans, hist, seed_flags, T, wout);
+        else
+            hipLaunchKernelGGL((kabsch_sums_kernel<true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k, sums, rg,
+                               seed_trans, nullptr, nullptr, 0, nullptr);
     } else {
-        hipLaunchKernelGGL(kabsch_sums_kernel<false>, dim3((S + wpb - 1) / wpb, B), dim3(64 * wpb), 0, s, src, tgt, knn,
-                           weights, N, S, k, sums, rg, seed_trans);
+        if (fin)
+            hipLaunchKernelGGL((kabsch_sums_kernel<false, true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k,
+                               sums, rg, seed_trans, hist, seed_flags, T, wout);
+        else
+            hipLaunchKernelGGL((kabsch_sums_kernel<false>), grid, block, 0, s, src, tgt, knn, weights, N, S, k, sums,
+                               rg, seed_trans, nullptr, nullptr, 0, nullptr);
         hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, S, seed_trans, rg);
     }
     hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
@@ -1134,17 +1170,14 @@ hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn,
 }
 
 // ------------------------------------------------------------- a10 best
-__global__ __launch_bounds__(256) void select_best_kernel(const float *__restrict__ src,
-                                                          const float *__restrict__ tgt,
-                                                          const float *__restrict__ seed_trans,
-                                                          const int *__restrict__ counts, int Nstr, int Sstr,
-                                                          float tau, float *__restrict__ fitness,
-                                                          int *__restrict__ best_out,
-                                                          float *__restrict__ trans,
-                                                          float *__restrict__ labels, Ragged rg,
-                                                          const float *__restrict__ conf, int *__restrict__ range) {
-    __shared__ int wbest[4], wcnt[4];
-    __shared__ float Ts[16];
+// One 256-thread workgroup per pair: the range guard, the first argmax of the
+// inlier counts, the best hypothesis into Ts (LDS) and trans, its labels.
+// Returns false for a pair the range guard flagged (workgroup-uniform).
+PDSC_DEV bool select_best_wg(const float *__restrict__ src, const float *__restrict__ tgt,
+                             const float *__restrict__ seed_trans, const int *__restrict__ counts, int Nstr, int Sstr,
+                             float tau, float *__restrict__ fitness, int *__restrict__ best_out,
+                             float *__restrict__ trans, float *__restrict__ labels, const Ragged &rg,
+                             const float *__restrict__ conf, int *__restrict__ range, int *wbest, int *wcnt, float *Ts) {
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int N = rg.n(b, Nstr), S = rg.s(b, Sstr);  // this pair's sizes; Nstr, Sstr: the strides
     if (conf) {
@@ -1158,7 +1191,7 @@ __global__ __launch_bounds__(256) void select_best_kernel(const float *__restric
         if (bad) {
             if (tid < 16) trans[(size_t)b * 16 + tid] = __builtin_nanf("");
             for (int n = tid; n < Nstr; n += 256) labels[(size_t)b * Nstr + n] = 0.0f;
-            return;  // workgroup-uniform
+            return false;  // workgroup-uniform
         }
     }
     int bc = -1, bi = 0x7fffffff;
@@ -1198,6 +1231,22 @@ __global__ __launch_bounds__(256) void select_best_kernel(const float *__restric
         labels[(size_t)b * Nstr + n] = (L2 < tau) ? 1.0f : 0.0f;
     }
     for (int n = N + tid; n < Nstr; n += 256) labels[(size_t)b * Nstr + n] = 0.0f;  // a ragged pair's padding
+    return true;
+}
+
+__global__ __launch_bounds__(256) void select_best_kernel(const float *__restrict__ src,
+                                                          const float *__restrict__ tgt,
+                                                          const float *__restrict__ seed_trans,
+                                                          const int *__restrict__ counts, int Nstr, int Sstr,
+                                                          float tau, float *__restrict__ fitness,
+                                                          int *__restrict__ best_out,
+                                                          float *__restrict__ trans,
+                                                          float *__restrict__ labels, Ragged rg,
+                                                          const float *__restrict__ conf, int *__restrict__ range) {
+    __shared__ int wbest[4], wcnt[4];
+    __shared__ float Ts[16];
+    select_best_wg(src, tgt, seed_trans, counts, Nstr, Sstr, tau, fitness, best_out, trans, labels, rg, conf, range,
+                   wbest, wcnt, Ts);
 }
 
 hipError_t launch_select_best(const float *src, const float *tgt, const float *seed_trans,
@@ -1280,18 +1329,13 @@ PDSC_DEV void block_rigid_h(const float *__restrict__ A, const float *__restrict
 }
 
 // ---------------------------------------------------- a11 post-refinement
-__global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ trans,
-                                                         const float *__restrict__ src,
-                                                         const float *__restrict__ tgt, int Nstr,
-                                                         float thr, Ragged rg, const int *__restrict__ range) {
-    __shared__ float red[RW][9];
-    __shared__ float Ts[16];
+// The refinement of pair blockIdx.x from the pose in Ts (LDS, every thread's
+// view current), written to trans[b] at the end.
+PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *__restrict__ src,
+                             const float *__restrict__ tgt, int Nstr, float thr, const Ragged &rg, float (*red)[9]) {
     const int b = blockIdx.x, tid = threadIdx.x;
-    if (range && range[b]) return;  // a pair the range guard flagged keeps its NaN pose (workgroup-uniform)
     const int N = rg.n(b, Nstr);  // this pair's correspondences; Nstr: the stride
     const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
-    if (tid < 16) Ts[tid] = trans[(size_t)b * 16 + tid];
-    __syncthreads();
     int prev = 0;
     for (int it = 0; it < 20; ++it) {
         float T[12];
@@ -1337,6 +1381,45 @@ __global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ tra
         __syncthreads();
     }
     if (tid < 16) trans[(size_t)b * 16 + tid] = Ts[tid];
+}
+
+__global__ __launch_bounds__(RB) void post_refine_kernel(float *__restrict__ trans,
+                                                         const float *__restrict__ src,
+                                                         const float *__restrict__ tgt, int Nstr,
+                                                         float thr, Ragged rg, const int *__restrict__ range) {
+    __shared__ float red[RW][9];
+    __shared__ float Ts[16];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (range && range[b]) return;  // a pair the range guard flagged keeps its NaN pose (workgroup-uniform)
+    if (tid < 16) Ts[tid] = trans[(size_t)b * 16 + tid];
+    __syncthreads();
+    post_refine_wg(Ts, trans, src, tgt, Nstr, thr, rg, red);
+}
+
+// select_best + post_refine of one pair in one launch (the testing forward):
+// the same two workgroup bodies back to back, the best pose handed over in LDS.
+static_assert(RB == 256, "select_best_wg runs 256 threads");
+__global__ __launch_bounds__(RB) void best_refine_kernel(const float *__restrict__ src, const float *__restrict__ tgt,
+                                                         const float *__restrict__ seed_trans,
+                                                         const int *__restrict__ counts, int Nstr, int Sstr,
+                                                         float tau, float thr, float *__restrict__ trans,
+                                                         float *__restrict__ labels, Ragged rg,
+                                                         const float *__restrict__ conf, int *__restrict__ range) {
+    __shared__ int wbest[4], wcnt[4];
+    __shared__ float Ts[16];
+    __shared__ float red[RW][9];
+    if (!select_best_wg(src, tgt, seed_trans, counts, Nstr, Sstr, tau, nullptr, nullptr, trans, labels, rg, conf, range,
+                        wbest, wcnt, Ts))
+        return;  // (workgroup-uniform) the range guard's NaN pose stays
+    post_refine_wg(Ts, trans, src, tgt, Nstr, thr, rg, red);
+}
+
+hipError_t launch_best_refine(const float *src, const float *tgt, const float *seed_trans, const int *counts, int B,
+                              int N, int S, float tau, float thr, float *trans, float *labels, hipStream_t s,
+                              Ragged rg, const float *conf, int *range) {
+    hipLaunchKernelGGL(best_refine_kernel, dim3(B), dim3(RB), 0, s, src, tgt, seed_trans, counts, N, S, tau, thr, trans,
+                       labels, rg, conf, range);
+    return hipGetLastError();
 }
 
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,

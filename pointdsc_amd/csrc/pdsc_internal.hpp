@@ -251,9 +251,13 @@ hipError_t launch_nsm_seed(const void *feats, bool f32, const float *src, const 
 hipError_t launch_nsm_finish(const float *hist, const unsigned *seed_flags, int B, int S, int k, int T, bool batch_global,
                              float *weights, int *iters_used, hipStream_t s, Ragged rg = {});
 // sums: scratch [B][S][15]
+// hist != NULL (the testing forward): the NSM weights are finished inside the
+// first launch (nsm_finish's arithmetic, per-pair allclose over hist /
+// seed_flags) and written to wout; `weights` is then not read.
 hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn, const float *weights,
                              int B, int N, int S, int k, float tau, float *seed_trans, int *counts,
-                             float *sums, hipStream_t s, Ragged rg = {});
+                             float *sums, hipStream_t s, Ragged rg = {}, const float *hist = nullptr,
+                             const unsigned *seed_flags = nullptr, int T = 0, float *wout = nullptr);
 // conf / range (both may be null): the forward's fp16 range guard -- a pair
 // whose logits conf[b, :n] hold a non-finite value gets range[b] = 1 (else 0),
 // final_trans all NaN and labels 0; post_refine leaves such a pair alone.
@@ -263,6 +267,10 @@ hipError_t launch_select_best(const float *src, const float *tgt, const float *s
                               const float *conf = nullptr, int *range = nullptr);
 hipError_t launch_post_refine(float *trans, const float *src, const float *tgt, int B, int N, float thr,
                               hipStream_t s, Ragged rg = {}, const int *range = nullptr);
+// launch_select_best (fitness and best not written) + launch_post_refine in one launch
+hipError_t launch_best_refine(const float *src, const float *tgt, const float *seed_trans, const int *counts, int B,
+                              int N, int S, float tau, float thr, float *trans, float *labels, hipStream_t s,
+                              Ragged rg = {}, const float *conf = nullptr, int *range = nullptr);
 hipError_t launch_rigid(const float *A, const float *Bp, const float *w, int nb, int n, float *trans,
                         hipStream_t s);
 

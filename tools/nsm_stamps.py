@@ -53,6 +53,7 @@ def main():
            "wave_us_mean": float(np.mean(st[:, 17] - st[:, 16]) / 100.0),
            "launch_span_us": float((st[:, 17].max() - r0) / 100.0),
            "start_us_pctl": [float(np.percentile((st[:, 16] - r0) / 100.0, q)) for q in (0, 25, 50, 75, 100)],
+           "end_us_pctl": [float(np.percentile((st[:, 17] - r0) / 100.0, q)) for q in (0, 25, 50, 75, 90, 100)],
            "segments_us": seg}
     print(json.dumps(rep, indent=1))
 

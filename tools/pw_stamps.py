@@ -47,6 +47,9 @@ def main():
     assert L.pdsc_diag_att_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes)) == 0
     st = buf.reshape(ST_WGS, 4, ST_PER_WAVE).astype(np.int64)
     rep = {}
+    # wave 0 of each stamped workgroup (small-batch launches run 1-, 2- or 8-wave
+    # workgroups; only waves 0-3 stamp, and wave 0 always exists)
+    st = st[:, :1, :]
     pw = st[(st[:, :, 150] > 0).all(1) & (st[:, :, 159] > 0).all(1)]
     if len(pw):
         ghz = np.median((pw[:, :, 159] - pw[:, :, 150]) / (pw[:, :, 187] - pw[:, :, 186]) * 0.1)
