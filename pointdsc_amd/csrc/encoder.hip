@@ -338,10 +338,55 @@ hipError_t launch_split_qkv(const float *q, const float *k, const float *v, int 
 // (the split loop's loads otherwise wait for each other: 10.6 of a single
 // N = 1000 pair's 25 us pw_mid launch went to the 16-split combine).  Same
 // arithmetic, same order as the one-load-per-split loop.
+#ifndef PDSC_C16_ONE
+#define PDSC_C16_ONE 8  // A/B build knob (-DPDSC_C16_ONE=0: the chunked loads only)
+#endif
+constexpr int C16_ONE = PDSC_C16_ONE;  // combine16: up to this many splits in one batch of loads (r06)
 template <bool F32>
 PDSC_DEV void combine16(const float *__restrict__ opart, const float *__restrict__ ml, int b,
                         int nsplit, int Npad, int row, int d0, float out[16]) {
     const float *mlb = ml + ((size_t)b * nsplit * Npad + row) * 2;  // split s: mlb[s * Npad * 2 + {0, 1}]
+    if (nsplit <= C16_ONE) {
+        // every split's m, l and 16 channels in ONE batch of loads (one round
+        // trip to the partials the attention launch just left in other XCDs'
+        // caches, instead of three), the maximum from the loaded m's: the same
+        // operations in the same order as the chunked loop below
+        f32x2 mlv[C16_ONE > 0 ? C16_ONE : 1];
+        f32x4 ov[C16_ONE > 0 ? C16_ONE : 1][4];
+#pragma unroll
+        for (int j = 0; j < C16_ONE; ++j) {
+            if (j < nsplit) {
+                const size_t base = (size_t)(b * nsplit + j) * Npad + row;
+                mlv[j] = *reinterpret_cast<const f32x2 *>(ml + base * 2);
+                const float *ob = opart + (base - row) * CH;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const size_t o = F32 ? (size_t)row * CH + d0 + 4 * i : h3_opart_off(row, d0 + 4 * i);
+                    ov[j][i] = *reinterpret_cast<const f32x4 *>(ob + o);
+                }
+            }
+        }
+        float mstar = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < C16_ONE; ++j)
+            if (j < nsplit) mstar = fmaxf(mstar, mlv[j][0]);
+        float L = 0.0f;
+        f32x4 acc[4] = {};
+#pragma unroll
+        for (int j = 0; j < C16_ONE; ++j) {
+            if (j < nsplit) {
+                const float w = expf(mlv[j][0] - mstar);
+                L += w * mlv[j][1];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] += w * ov[j][i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) out[4 * i + e] = acc[i][e] / L;
+        return;
+    }
     float mstar = -INFINITY;
     for (int s0 = 0; s0 < nsplit; s0 += 8) {
         float mv[8];
@@ -1308,6 +1353,8 @@ PDSC_DEV void w2_combine(const float *__restrict__ opart, const float *__restric
     f32x4 acc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    // (r06: both splits of a pair issued before either is used measured no
+    // faster at 8 x 5000, 4.34 vs 4.33 ms per forward: not kept)
     for (int s = 0; s < nsplit; ++s) {
         const size_t base = (size_t)(b * nsplit + s) * Npad + row;
         const float ms = ml[base * 2];
