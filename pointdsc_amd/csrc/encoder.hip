@@ -528,7 +528,7 @@ hipError_t launch_combine_rows(const float *opart, const float *ml, int B, int N
 // outputs): each wave owns column tiles and computes BOTH row tiles, so every
 // weight fragment feeds two MFMAs; narrow layers (32/64 outputs): one
 // (row tile, column tile) per wave so all four waves stay busy.
-enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3 };
+enum Epi { EPI_BIAS = 0, EPI_RELU = 1, EPI_BN_RELU = 2, EPI_RESID = 3, EPI_RESID_R = 4 };
 
 // ReLU that keeps NaN (torch.relu(nan) = nan; fmaxf(nan, 0) = 0).  The fp16
 // range guard relies on it: a 3xfp16 operand beyond fp16's range (hi = inf,
@@ -590,7 +590,7 @@ PDSC_DEV void split8(const float *x, int h, f16x8 &hi, f16x8 &lo) {
 template <int IN, int OUT, int EPI, int NRT, bool F32>
 PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, const float *__restrict__ pk,
                            const DenseOff &off, int rt0, int ct, float *Y, int ystr, const float *__restrict__ resid,
-                           int lane) {
+                           int lane, const float *rres = nullptr) {
     const int h = lane >> 5, l32 = lane & 31;
     f32x16 acc[NRT];
 #pragma unroll
@@ -631,6 +631,7 @@ PDSC_DEV void dense_tile_w(const float *X, int xstr, const WPanel<IN, F32> &wp, 
             if (EPI == EPI_BN_RELU) y = relu_nan(y * al + be);  // eval BN as torch folds it, ReLU
             if (EPI == EPI_RELU) y = relu_nan(y);
             if (EPI == EPI_RESID) y = resid[row * CH + j] + y;      // res = feat + message (:44)
+            if (EPI == EPI_RESID_R) y = rres[16 * i + r] + y;       // the same, rows loaded ahead (NRT = 1)
             Y[row * ystr + j] = y;
         }
 }
@@ -1029,6 +1030,89 @@ PDSC_DEV void message_resid(float *A, float *C, float *R, const float *__restric
     CH_STAMP(154);
 }
 
+// pw_mid's chain for the 8-wave workgroups of a Q / K / V split (three
+// workgroups per 32-point tile, `only` = blockIdx.z), each wave's weight panel
+// loaded a phase ahead of its layer instead of at its start (the single pair's
+// chain is a sequence of L2 round trips: every layer of the message chain paid
+// one before its MFMAs).  Roles: fc0 on waves 4-5 and fc3 on waves 6-7 (panels
+// loaded before the combine), fc6 on waves 0-3 (panel and residual rows loaded
+// before the combine), PointCN on waves 4-7 (panel loaded once fc0 / fc3 are
+// done, during fc6), the projection on waves 0-3 (panel loaded after fc6,
+// during PointCN).  Every output tile is the same dense_tile_w / dense_split
+// arithmetic as message_resid + pcn_qkv8: the same bits.
+PDSC_DEV void mid_split8(float *XA, float *XB, const float *__restrict__ pk, const PwMsg &m, const PwDense4 &d,
+                         const float *__restrict__ opart, const float *__restrict__ ml, int b, int nsplit, int Npad,
+                         int p0, const float *__restrict__ feat_rows, float *__restrict__ feat,
+                         _Float16 *__restrict__ Q, _Float16 *__restrict__ K, _Float16 *__restrict__ V,
+                         float *__restrict__ vexp, int only, int tid, int wave, int lane) {
+    constexpr int PTT = 32;
+    float *XC = XB;
+    const int w4 = wave & 3, h = lane >> 5, l32 = lane & 31;
+    WPanel<CH, false> pa;   // fc0 (waves 4-5), then PointCN (waves 4-7) / the projection (waves 0-3)
+    WPanel<CH2, false> pb;  // fc3 (waves 6-7) / fc6 (waves 0-3)
+    float res[16];          // fc6's residual rows (waves 0-3)
+    if (wave >= 6)
+        load_wpanel<CH2, CH2, false>(pk, m.fc3, wave - 6, lane, pb);
+    else if (wave >= 4)
+        load_wpanel<CH, CH2, false>(pk, m.fc0, wave - 4, lane, pa);
+    asm volatile("" ::: "memory");
+    if (tid < 256) {
+        combine_tile<PTT, false>(opart, ml, b, nsplit, Npad, p0, XA, tid);
+        // (after the combine: its loads and these do not share the register file)
+        load_wpanel<CH2, CH, false>(pk, m.fc6, wave, lane, pb);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) res[r] = feat_rows[acc_row(r, h) * CH + wave * 32 + l32];
+    }
+    asm volatile("" ::: "memory");
+    __syncthreads();
+    CH_STAMP(151);
+    if (wave == 4 || wave == 5)  // fc0: XA -> XC
+        dense_tile_w<CH, CH2, EPI_BN_RELU, 1, false>(XA, S132, pa, pk, m.fc0, 0, wave - 4, XC, S68, nullptr, lane);
+    __syncthreads();
+    CH_STAMP(152);
+    if (wave >= 4) load_wpanel<CH, CH, false>(pk, d.pcn, w4, lane, pa);  // (waves 4-5 are done with fc0's)
+    asm volatile("" ::: "memory");
+    if (wave >= 6)  // fc3: XC -> XA
+        dense_tile_w<CH2, CH2, EPI_BN_RELU, 1, false>(XC, S68, pb, pk, m.fc3, 0, wave - 6, XA, S68, nullptr, lane);
+    __syncthreads();
+    CH_STAMP(153);
+    if (wave < 4)  // fc6 + residual: XA -> XB
+        dense_tile_w<CH2, CH, EPI_RESID_R, 1, false>(XA, S68, pb, pk, m.fc6, 0, wave, XB, S132, nullptr, lane, res);
+    __syncthreads();
+    CH_STAMP(154);
+    if (wave < 4) load_wpanel<CH, CH, false>(pk, only == 0 ? d.q : (only == 1 ? d.k : d.v), wave, lane, pa);
+    asm volatile("" ::: "memory");
+    if (wave >= 4)  // PointCN: XB -> XA
+        dense_tile_w<CH, CH, EPI_BN_RELU, 1, false>(XB, S132, pa, pk, d.pcn, 0, w4, XA, S132, nullptr, lane);
+    __syncthreads();  // XA complete; XB is dead (it now holds the split copy of XA)
+    CH_STAMP(155);
+    char *Xs = reinterpret_cast<char *>(XB);
+    split_tile<PTT, 512>(XA, S132, Xs, tid);
+    if (only == 0) store_rows<PTT, 512>(XA, S132, feat, p0, PTT, tid);
+    __syncthreads();
+    CH_STAMP(156);
+    CH_STAMP(157);
+    CH_STAMP(158);
+    if (only == 0) {
+        if (wave < 4) dense_split<SPLIT_Q, 1>(Xs, pa, pk, d.q, wave, Q, p0, lane);
+    } else if (only == 1) {
+        if (wave < 4) dense_split<SPLIT_K, 1>(Xs, pa, pk, d.k, wave, K, p0, lane);
+    } else {
+        dense_split<SPLIT_V, 1>(Xs, pa, pk, d.v, w4, V, p0, lane, XA, vexp, wave < 4);  // XA is dead
+    }
+    CH_STAMP(159);
+}
+
+// A/B knob (measurement only): PDSC_PW_PREFETCH=0 runs the Q / K / V split
+// chain without the panel prefetch (message_resid + pcn_qkv8).
+static bool pw_prefetch_on() {
+    static const bool off = [] {
+        const char *e = getenv("PDSC_PW_PREFETCH");
+        return e && e[0] == '0';
+    }();
+    return !off;
+}
+
 template <int PTT, bool F32, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(const float *__restrict__ pk, PwMsg m, PwDense4 d,
                                                      const float *__restrict__ opart,
@@ -1037,7 +1121,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(cons
                                                      float *__restrict__ feat,
                                                      _Float16 *__restrict__ Q, _Float16 *__restrict__ K,
                                                      _Float16 *__restrict__ V, float *__restrict__ vexp,
-                                                     int diag_delay) {
+                                                     int diag_delay, int prefetch) {
     // feat_in != feat: with gridDim.z == 3 the three workgroups of a point tile
     // read feat_in's rows as fc6's residual while the z = 0 one writes feat
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1054,6 +1138,15 @@ __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void pw_mid_kernel(cons
     ATT_RSTAMP(stp, 186);
     ATT_STAMP(stp, 150);
 #endif
+    if constexpr (NWV == 8 && PTT == 32 && !F32) {
+        if (prefetch && gridDim.z == 3) {  // workgroup-uniform
+            mid_split8(XA, XB, pk, m, d, opart, ml, b, nsplit, Npad, p0, feat_in + boff + (size_t)p0 * CH, feat + boff,
+                       Q + 2 * boff, K + 2 * boff, V + 2 * boff, vexp + (size_t)b * (Npad / 32), (int)blockIdx.z, tid,
+                       wave, lane);
+            ATT_RSTAMP(stp, 187);
+            return;
+        }
+    }
     if (tid < 256) combine_tile<PTT, F32>(opart, ml, b, nsplit, Npad, p0, XA, tid);
     __syncthreads();
     ATT_STAMP(stp, 151);
@@ -2017,11 +2110,11 @@ hipError_t launch_pw_mid(const float *packed, const PackLayout &lay, int layer, 
         hipLaunchKernelGGL((pw_mid_kernel<32, false, 8>), dim3(Npad / 32, B, pw_qkv_split(B, Npad) ? 3 : 1), dim3(512),
                            pw_lds<32>(), s, packed,
                            msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit, N, Npad, feat_in,
-                           feat, Q, K, V, vexp, delay);
+                           feat, Q, K, V, vexp, delay, (int)pw_prefetch_on());
         return hipGetLastError();
     }
     PW_LAUNCH(pw_mid_kernel, Npad, packed, msg3(lay.layer[layer]), dense4(lay.layer[layer + 1]), opart, ml, nsplit,
-              N, Npad, feat_in, feat, Q, K, V, vexp, 0);
+              N, Npad, feat_in, feat, Q, K, V, vexp, 0, 0);
     return hipGetLastError();
 }
 
