@@ -659,7 +659,11 @@ def main():
             cpu = {"value": round(n_done * N / t_c, 1), "unit": "correspondences/s", "cores": cores,
                    "kind": "port",
                    "sample": f"{n_done} of the {P} bench pairs (N={N}) through oracle.pdsc_oracle."
-                             f"forward_testing (numpy/BLAS + C), {t_c:.1f} s"}
+                             f"forward_testing (numpy/BLAS + C), {t_c:.1f} s",
+                   "note": "the oracle port, not the reference: it is slower than the reference's own torch "
+                           "CPU forward, which SURVEY.md section 6 measured at about 19k correspondences/s "
+                           "(N = 1000, 8 threads) in the build container; the reference itself does not "
+                           "travel to the GPU box"}
 
         result = {
             "metric": "correspondence-pairs/sec through NSM (N=1k/5k) at 1/2/4/8 GPUs; 3DMatch recall parity",

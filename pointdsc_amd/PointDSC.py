@@ -330,8 +330,11 @@ class PointDSC(nn.Module):
         general path, which raises the precise error or re-runs a marked pair in
         exact fp32 -- when the workspace is not cacheable or the pair is marked."""
         dev = src.device
-        corr_pos, src, tgt = (kernels._dev(corr_pos, "corr_pos"), kernels._dev(src, "src_keypts"),
-                              kernels._dev(tgt, "tgt_keypts"))
+        f32 = torch.float32
+        if not (corr_pos.dtype is f32 and src.dtype is f32 and tgt.dtype is f32 and corr_pos.is_cuda and tgt.is_cuda
+                and corr_pos.is_contiguous() and src.is_contiguous() and tgt.is_contiguous()):
+            corr_pos, src, tgt = (kernels._dev(corr_pos, "corr_pos"), kernels._dev(src, "src_keypts"),
+                                  kernels._dev(tgt, "tgt_keypts"))
         cfg, pk = self.pdsc_config(), self.packed_weights()
         kernels._check_inputs(cfg, corr_pos, src, tgt)
         N = src.shape[1]
@@ -356,8 +359,8 @@ class PointDSC(nn.Module):
         ws = wsc.get(wkey)
         if ws is None or ws.numel() < nb:  # another model size / N grew the stream's workspace meanwhile
             ws = self._workspace(cfg, 1, N, dev)
-        trans = torch.empty((1, 4, 4), dtype=torch.float32, device=dev)
-        labels = torch.empty((1, N), dtype=torch.float32, device=dev)
+        out = torch.empty(16 + N, dtype=torch.float32, device=dev)  # one allocation, two views
+        trans, labels = out[:16].view(1, 4, 4), out[16:].view(1, N)
         wp = ws.data_ptr()
         _lib.check(fwd(cfgp, pk.data_ptr(), corr_pos.data_ptr(), src.data_ptr(), tgt.data_ptr(), 1, N,
                        trans.data_ptr(), labels.data_ptr(), None, None, wp, nb, sp), "pdsc_forward_testing")

@@ -347,17 +347,28 @@ PDSC_DEV AttnBlock attention_h3_block(const AttnGridH3 &g, bool xcd) {
 // ahead.  Measured (A/B, one box): 4 x 5000 forward 2.405 vs 2.460 ms; on the
 // single pair's 2-tile splits 0.419 vs 0.417 ms, so those keep the plain loop.
 // The same arithmetic on the same operands: bit-identical either way.
-template <int NW, bool PACKED, bool EARLY = false>
+// WS > 0 (attention_h3_ws_kernel, the tiny plan): the workgroup's WS waves
+// share ONE block of 32 queries and split the key split's tiles between them
+// (wave w: the w-th of WS contiguous runs); each wave stages its own tiles into
+// a single LDS slot of its own (h3smem + w (KTB + VTB)) with no workgroup
+// barrier, and the caller merges the waves' (O, m, l) (NW must be 1).
+template <int NW, bool PACKED, bool EARLY = false, int WS = 0>
 PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks,
                                 const _Float16 *__restrict__ Vs, const float *__restrict__ vexp,
                                 const float *__restrict__ M, const AttnGridH3 &g, const AttnBlock &blk, char *h3smem,
                                 int wave, int lane, f32x16 (&O)[4], float &m_run, float &l_run) {
+    static_assert(WS == 0 || (NW == 1 && !EARLY), "wave-split: one 32-query block, the plain loop");
     const int b = blk.b, qb = blk.qb, split = blk.split;
     const int N = g.n(b), Npad = g.Npad;  // this pair's keys; the batch's row stride
     const int h = lane >> 5, l32 = lane & 31;
-    const int q0 = qb * (NW * 32) + wave * 32;
+    const int q0 = WS ? qb * 32 : qb * (NW * 32) + wave * 32;
     const int nst = (N + H3_TILE - 1) / H3_TILE;
-    const int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
+    int st0 = split * g.sps, st1 = min(nst, st0 + g.sps);
+    if constexpr (WS > 0) {  // this wave's run of the split's tiles (wave-uniform)
+        const int tpw = (st1 - st0 + WS - 1) / WS, a = min(st1, st0 + wave * tpw);
+        st1 = min(st1, a + tpw);
+        st0 = a;
+    }
     const int qq = q0 + l32;
     const bool active = q0 < Npad;
 
@@ -383,11 +394,11 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     const __amdgpu_buffer_rsrc_t rK = h3_rsrc(Kp, (uint32_t)Npad * H3_ROWB), rV = h3_rsrc(Vp, (uint32_t)Npad * H3_ROWB);
 #endif
     auto stage = [&](int st, int slot) {
-        char *dst = h3smem + slot * (H3_KTB + H3_VTB);
+        char *dst = h3smem + (WS ? wave : slot) * (H3_KTB + H3_VTB);
         constexpr int PIECES = (H3_KTB + H3_VTB) / 1024;
 #pragma unroll
         for (int i = 0; i < PIECES / NW; ++i) {
-            const int piece = wave * (PIECES / NW) + i;  // wave-uniform (SGPR)
+            const int piece = WS ? i : wave * (PIECES / NW) + i;  // wave-uniform (SGPR)
 #if ATT_BUFDMA
             // the piece's offset in the SGPR operand: no per-piece address VALU
             if (piece < H3_KTB / 1024)
@@ -593,7 +604,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // Immediate (gfx9 simm16): vmcnt[3:0] | expcnt(7) << 4 | lgkmcnt(0) << 8.
     auto sync = [&] {
         __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
+        if constexpr (WS == 0) __builtin_amdgcn_s_barrier();  // (WS: the wave's own slot only)
     };
 
     // (Measured and reverted: M and the exponent loaded by inline asm with an
@@ -601,7 +612,9 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // included, because it does not count LDS-DMA -- issued at the tile start
     // or at the end of the previous tile: no faster, and the compiler copies
     // asm-loaded registers before the wait.  DESIGN.md section 7.)
-    auto slot_base = [&](int st) { return h3smem + ((st - st0) % H3_NSLOT) * (H3_KTB + H3_VTB); };
+    auto slot_base = [&](int st) {
+        return h3smem + (WS ? wave : (st - st0) % H3_NSLOT) * (H3_KTB + H3_VTB);
+    };
     float mvA[16], evA;  // EARLY: the next tile's M, loaded a tile ahead
     if (st0 < st1) {
         stage(st0, 0);
@@ -625,6 +638,10 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             // tile st0 + 1 went out before the loop; tile st + 1's slot held tile
             // st - 1, released by the barrier that ended iteration st - 1
             if (st > st0 && st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
+        } else if constexpr (WS > 0) {
+            // one slot per wave: tile st + 1 is staged after tile st's reads (below)
+            load_m(st * H3_TILE, mv, ev);
+            if (st > st0) sync();  // tile st landed (staged at the end of the previous iteration)
         } else {
             load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
             if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
@@ -634,7 +651,14 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
         ATT_STAMP(stp, si + 3);
         pv(slot_base(st) + H3_KTB, ph, pl);
         ATT_STAMP(stp, si + 4);
-        sync();
+        if constexpr (WS > 0) {
+            if (st + 1 < st1) {
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this tile's LDS reads returned
+                stage(st + 1, 0);
+            }
+        } else {
+            sync();
+        }
         ATT_STAMP(stp, si + 5);
     }
     l_run = halves_sum(l_run);
@@ -677,6 +701,79 @@ __global__ __launch_bounds__(NW * 64, 2) void attention_h3_kernel(
         // partial max in natural-log units (the p's carry the 2^PSHIFT factor)
         ml[(obase + qq) * 2] = (m_run - (float)H3_PSHIFT) * 0.6931471805599453f;
         ml[(obase + qq) * 2 + 1] = l_run;
+    }
+}
+
+// The tiny plan's split-K attention with the split's key tiles spread over the
+// workgroup's WS waves (attention_h3_core's WS mode; one 32-query block per
+// workgroup): each wave runs its run of tiles alone on its SIMD (no partner
+// wave, no workgroup barrier per tile), then the waves' (O, m, l) are merged
+// through LDS into the workgroup's ONE partial -- the split count and the
+// partials the pointwise kernel combines stay those of the one-wave plan.
+//   O = sum_w 2^(m_w - m*) O_w,  l = sum_w 2^(m_w - m*) l_w,  m = m* = max_w m_w
+// (waves in ascending order; an empty run has m = -inf: weight 0).  LDS: WS
+// single-tile slots of 32 KiB, each wave's slot reused for its merge record.
+template <int WS>
+constexpr size_t attention_h3_ws_lds_bytes() { return (size_t)WS * (H3_KTB + H3_VTB); }
+
+template <int WS, bool PACKED>
+__global__ __launch_bounds__(WS * 64) void attention_h3_ws_kernel(
+    const _Float16 *__restrict__ Qs, const _Float16 *__restrict__ Ks, const _Float16 *__restrict__ Vs,
+    const float *__restrict__ vexp, const float *__restrict__ M, AttnGridH3 g, float *__restrict__ opart,
+    float *__restrict__ ml) {
+    extern __shared__ __attribute__((aligned(16))) char h3smem[];
+    const AttnBlock blk = attention_h3_block(g, true);
+    if (blk.qb * 32 >= g.n(blk.b)) return;  // past a ragged pair's end (workgroup-uniform)
+    const int b = blk.b, split = blk.split, Npad = g.Npad;
+    const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, h = lane >> 5;
+    const int q0 = blk.qb * 32, qq = q0 + (lane & 31);
+    f32x16 O[4];
+    float m_run, l_run;
+    attention_h3_core<1, PACKED, false, WS>(Qs, Ks, Vs, vexp, M, g, blk, h3smem, wave, lane, O, m_run, l_run);
+    // merge record in this wave's own slot: O[t][r] at ((16 t + r) * 64 + lane), then m, l
+    float *rec = reinterpret_cast<float *>(h3smem + wave * (H3_KTB + H3_VTB));
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's last LDS reads of its slot returned
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rec[(16 * t + r) * 64 + lane] = O[t][r];
+    rec[4096 + lane] = m_run;
+    rec[4096 + 64 + lane] = l_run;
+    __syncthreads();
+    if (q0 >= Npad) return;
+    float mw[WS], ms = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < WS; ++w) {
+        mw[w] = reinterpret_cast<const float *>(h3smem + w * (H3_KTB + H3_VTB))[4096 + lane];
+        ms = fmaxf(ms, mw[w]);
+    }
+    float a[WS];
+#pragma unroll
+    for (int w = 0; w < WS; ++w) a[w] = ms == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mw[w] - ms);
+    const size_t obase = (size_t)(b * g.nsplit + split) * Npad;
+    float *Ob = opart + obase * CH + (size_t)(q0 >> 5) * (H3_TILE * CH) + 4 * lane;
+    for (int t = wave; t < 4; t += WS) {  // this wave's output tiles (registers 4q .. 4q+3 -> block 4t + q)
+        float acc[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int w = 0; w < WS; ++w) {
+            const float *rw = reinterpret_cast<const float *>(h3smem + w * (H3_KTB + H3_VTB));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = __builtin_fmaf(a[w], rw[(16 * t + r) * 64 + lane], acc[r]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<f32x4 *>(Ob + (4 * t + q) * 256) = f32x4{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+    }
+    if (wave == 0 && h == 0) {
+        float l = 0.0f;
+#pragma unroll
+        for (int w = 0; w < WS; ++w)
+            l = __builtin_fmaf(a[w], reinterpret_cast<const float *>(h3smem + w * (H3_KTB + H3_VTB))[4096 + 64 + lane], l);
+        // partial max in natural-log units (the p's carry the 2^PSHIFT factor)
+        ml[(obase + qq) * 2] = (ms - (float)H3_PSHIFT) * 0.6931471805599453f;
+        ml[(obase + qq) * 2 + 1] = l;
     }
 }
 

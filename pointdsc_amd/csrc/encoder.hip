@@ -171,6 +171,17 @@ static bool att_tiny(int B, int N) {
     }();
     return !off && (long)B * ((N + QB - 1) / QB) <= 8;
 }
+// The tiny plan's waves per workgroup splitting each key split's tiles
+// (attention_h3_ws_kernel): 4 (default), 2, or 1 = the one-wave kernel.
+// A/B knob PDSC_ATT_WS (measurement only).
+static int att_ws() {
+    static const int v = [] {
+        const char *e = getenv("PDSC_ATT_WS");
+        const int w = e ? atoi(e) : 4;
+        return (w == 1 || w == 2) ? w : 4;
+    }();
+    return v;
+}
 static AttnGridH3 prod_grid(int B, int N) {
     if (att_tiny(B, N)) return attention_h3_grid<1>(B, N, std::min(att_target(), 256));
     switch (att_nw(B, N)) {
@@ -301,6 +312,29 @@ hipError_t launch_attention(const void *q, const void *k, const void *v, const f
     g.rev = rg.po ? 0 : zigzag_rev(layer);
     if (g.Npad != Npad || g.nsplit != nsplit) return hipErrorInvalidValue;
     const int nw = att_nw(B, N);
+    // the tiny plan's tiles spread over the workgroup's waves where each split has
+    // at least 4 tiles (measured, ms per forward, 1 -> 4 waves: 1 x 1000 (4 tiles per
+    // split) 0.393 -> 0.377; 1 x 700 (2 tiles) 0.366 -> 0.371, 2 x 500 0.347 -> 0.351,
+    // so shorter splits keep the one-wave kernel; profiles/r06_ab_att_ws.log)
+    if (att_tiny(B, N) && att_ws() > 1 && g.sps >= 4) {
+        const dim3 grid(g.B * g.nqb * g.nsplit);
+        if (att_ws() == 2) {
+            if (m_packed)
+                hipLaunchKernelGGL((attention_h3_ws_kernel<2, true>), grid, dim3(128), attention_h3_ws_lds_bytes<2>(), s,
+                                   qs, ks, vs, vexp, M, g, opart, ml);
+            else
+                hipLaunchKernelGGL((attention_h3_ws_kernel<2, false>), grid, dim3(128), attention_h3_ws_lds_bytes<2>(),
+                                   s, qs, ks, vs, vexp, M, g, opart, ml);
+        } else {
+            if (m_packed)
+                hipLaunchKernelGGL((attention_h3_ws_kernel<4, true>), grid, dim3(256), attention_h3_ws_lds_bytes<4>(), s,
+                                   qs, ks, vs, vexp, M, g, opart, ml);
+            else
+                hipLaunchKernelGGL((attention_h3_ws_kernel<4, false>), grid, dim3(256), attention_h3_ws_lds_bytes<4>(),
+                                   s, qs, ks, vs, vexp, M, g, opart, ml);
+        }
+        return hipGetLastError();
+    }
     if (nw == 1) return launch_attention_h3<1>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
     if (nw == 2) return launch_attention_h3<2>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
     return launch_attention_h3<ATT_NW>(qs, ks, vs, vexp, M, m_packed, g, opart, ml, s);
