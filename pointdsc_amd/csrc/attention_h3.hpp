@@ -604,7 +604,9 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // Immediate (gfx9 simm16): vmcnt[3:0] | expcnt(7) << 4 | lgkmcnt(0) << 8.
     auto sync = [&] {
         __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+#ifndef ATT_DIAG_NOBAR
         if constexpr (WS == 0) __builtin_amdgcn_s_barrier();  // (WS: the wave's own slot only)
+#endif
     };
 
     // (Measured and reverted: M and the exponent loaded by inline asm with an
