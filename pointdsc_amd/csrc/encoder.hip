@@ -159,10 +159,11 @@ static int att_nw(int B, int N) {
     return (long)B * ((N + QB - 1) / QB) <= 16 ? v : ATT_NW;
 }
 // The smallest batches (at most 8 query blocks of 128: a single pair to N =
-// 1024): one-wave workgroups whose key splits fill ONE round of 256 slots
-// (a 1000-key pair: 32 blocks x 8 splits of 4 tiles) instead of 16 blocks x 16
-// splits of 2 -- half the split partials, so pw_mid combines them itself
-// (use_precombine: fewer than 16 splits) and the combine_rows launch goes.
+// 1024): 32-query workgroups whose key splits fill ONE round of
+// att_tiny_slots() (128) workgroups (a 1000-key pair: 32 blocks x 4 splits of 8
+// tiles, run by attention_h3_ws_kernel's 4 waves) instead of 16 blocks x 16
+// splits of 2 -- a quarter of the split partials, so pw_mid combines them
+// itself (use_precombine: fewer than 16 splits) and the combine_rows launch goes.
 // A/B knob PDSC_ATT_TINY=0 (measurement only).
 static bool att_tiny(int B, int N) {
     static const bool off = [] {
@@ -182,8 +183,21 @@ static int att_ws() {
     }();
     return v;
 }
+// The tiny plan's slot target (one round of this many workgroups): 128 (ms per
+// forward, wave-split kernel, profiles/r06_ab_tiny_slots.log: 1 x 1000 0.374 at
+// 256 slots -> 0.366 at 128 (4 splits of 8 tiles, 2 per wave; half the partials
+// again) -> 0.385 at 96, 0.415 at 64; 2 x 500 0.342 -> 0.316; 1 x 700 0.362 ->
+// 0.345).  A/B knob PDSC_ATT_TINY_SLOTS (measurement only).
+static int att_tiny_slots() {
+    static const int v = [] {
+        const char *e = getenv("PDSC_ATT_TINY_SLOTS");
+        const int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 128;
+    }();
+    return v;
+}
 static AttnGridH3 prod_grid(int B, int N) {
-    if (att_tiny(B, N)) return attention_h3_grid<1>(B, N, std::min(att_target(), 256));
+    if (att_tiny(B, N)) return attention_h3_grid<1>(B, N, std::min(att_target(), att_tiny_slots()));
     switch (att_nw(B, N)) {
     case 1: return attention_h3_grid<1>(B, N, att_target());
     case 2: return attention_h3_grid<2>(B, N, att_target());

@@ -986,7 +986,10 @@ PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[
 // FIN (the testing forward): the seed's NSM weights are finished here, as
 // nsm_finish_kernel computes them (nsm_tstar over the pair's seeds, nsm_weight;
 // the same bits), and written to `weights` -- one launch fewer per forward.
-template <bool SOLVE, bool FIN = false>
+// COUNT (with SOLVE, small batches): the seed's wave then counts the inliers of
+// its own hypothesis over the pair's correspondences (count_inliers_kernel's
+// test, residual_sq < tau2, the same integer) -- one launch fewer.
+template <bool SOLVE, bool FIN = false, bool COUNT = false>
 __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restrict__ src,
                                                           const float *__restrict__ tgt,
                                                           const int *__restrict__ knn,
@@ -994,7 +997,8 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
                                                           int S, int k, float *__restrict__ sums, Ragged rg,
                                                           float *__restrict__ trans, const float *__restrict__ hist = nullptr,
                                                           const unsigned *__restrict__ seed_flags = nullptr, int T = 0,
-                                                          float *__restrict__ wout = nullptr) {
+                                                          float *__restrict__ wout = nullptr, float tau2 = 0.0f,
+                                                          int *__restrict__ counts = nullptr) {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
     const int s = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int Sb = rg.s(b, S);
@@ -1034,12 +1038,25 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
             if (lane == 3 * i + jj) out = h;
         }
     if constexpr (SOLVE) {
+        float T[16];
         if (lane == 0) {
             const float cA[3] = {cA0, cA1, cA2}, cB[3] = {cB0, cB1, cB2};
-            float T[16];
             kabsch_finish(Hs, cA, cB, T);
 #pragma unroll
             for (int e = 0; e < 16; ++e) trans[((size_t)b * S + s) * 16 + e] = T[e];
+        }
+        if constexpr (COUNT) {
+            // lane 0's pose to every lane, then the pair's correspondences 64 at a time
+            float Tb[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) Tb[e] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, T[e])));
+            const int n = rg.n(b, N);
+            int c = 0;
+            for (int j = lane; j < n; j += 64)
+                c += residual_sq(Tb, sb[3 * j], sb[3 * j + 1], sb[3 * j + 2], tb[3 * j], tb[3 * j + 1], tb[3 * j + 2]) <
+                     tau2;  // L2 < tau (:327-328)
+            c = wave_sum(c);
+            if (lane == 0) counts[(size_t)b * S + s] = c;
         }
         return;
     }
@@ -1148,13 +1165,16 @@ hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn,
     const int n = B * S;
     const dim3 grid((S + wpb - 1) / wpb, B), block(64 * wpb);
     const bool fin = hist != nullptr;
+    const float tau2 = sqrt_ge_threshold(tau);
     if (kabsch_small(n)) {
+        // the inlier count in the same launch (count_inliers_kernel's integers)
         if (fin)
-            hipLaunchKernelGGL((kabsch_sums_kernel<true, true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k,
-                               sums, rg, seed_trans, hist, seed_flags, T, wout);
+            hipLaunchKernelGGL((kabsch_sums_kernel<true, true, true>), grid, block, 0, s, src, tgt, knn, weights, N, S,
+                               k, sums, rg, seed_trans, hist, seed_flags, T, wout, tau2, counts);
         else
-            hipLaunchKernelGGL((kabsch_sums_kernel<true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k, sums, rg,
-                               seed_trans, nullptr, nullptr, 0, nullptr);
+            hipLaunchKernelGGL((kabsch_sums_kernel<true, false, true>), grid, block, 0, s, src, tgt, knn, weights, N, S,
+                               k, sums, rg, seed_trans, nullptr, nullptr, 0, nullptr, tau2, counts);
+        return hipGetLastError();
     } else {
         if (fin)
             hipLaunchKernelGGL((kabsch_sums_kernel<false, true>), grid, block, 0, s, src, tgt, knn, weights, N, S, k,
@@ -1165,7 +1185,7 @@ hipError_t launch_hypotheses(const float *src, const float *tgt, const int *knn,
         hipLaunchKernelGGL(kabsch_solve_kernel, dim3((n + 63) / 64), dim3(64), 0, s, sums, n, S, seed_trans, rg);
     }
     hipLaunchKernelGGL(count_inliers_kernel, dim3((S + HS - 1) / HS, B), dim3(256), 0, s, src, tgt,
-                       seed_trans, N, S, sqrt_ge_threshold(tau), counts, rg);
+                       seed_trans, N, S, tau2, counts, rg);
     return hipGetLastError();
 }
 
