@@ -478,7 +478,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     // load here is waited for with lgkmcnt(0) in the middle of the softmax)
     // QK^T + online softmax of one key tile -> this lane's P fragments (ph, pl)
     auto qk_softmax = [&](const char *Kl, int key0, float (&mv)[16], float ev, f16x8(&ph)[2], f16x8(&pl)[2],
-                          bool first) {
+                          bool first, auto after_qk) {
         // S^T[key][query] = sum_c K[key][c] Q[query][c]
         f32x16 S = zero16();
         f16x8 kf[3][2];
@@ -494,6 +494,7 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             S = mfma_h3(kf[j % 3][0], kf[j % 3][1], qh[j], ql[j], S);
             __builtin_amdgcn_sched_barrier(0);
         }
+        after_qk();  // (WS: the next tile's K into the K half of the wave's slot)
         // the softmax's VALU at raised issue priority (the partner wave on this
         // SIMD is then mostly in its MFMA phase): -1.8 % per fused launch, measured
         if (ATT_SOFTMAX_PRIO > 0) __builtin_amdgcn_s_setprio(ATT_SOFTMAX_PRIO);
@@ -617,6 +618,60 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
     auto slot_base = [&](int st) {
         return h3smem + (WS ? wave : (st - st0) % H3_NSLOT) * (H3_KTB + H3_VTB);
     };
+    if constexpr (WS > 0) {
+        // One slot per wave, its K and V halves refilled separately: tile t+1's K
+        // is staged once tile t's QK^T has read its K (hidden behind tile t's
+        // softmax and P.V), its M and V once P.V has read V (behind tile t+1's
+        // QK^T).  Waits: the 16 V pieces issued last may stay in flight at a
+        // tile's top, the next tile's 16 K pieces before P.V.
+        char *slot = h3smem + wave * (H3_KTB + H3_VTB);
+        auto stage_half = [&](int st, bool v) {  // 16 pieces of 1 KiB
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+#if ATT_BUFDMA
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(v ? rV : rK,
+                                                         (__attribute__((address_space(3))) void *)(slot + (v ? H3_KTB : 0) + i * 1024),
+                                                         16, 16 * lane, st * (v ? H3_VTB : H3_KTB) + i * 1024, 0, 0);
+#else
+                const char *src = (v ? Vp + (size_t)st * H3_VTB : Kp + (size_t)st * H3_KTB) + i * 1024;
+                __builtin_amdgcn_global_load_lds(src + 16 * lane, slot + (v ? H3_KTB : 0) + i * 1024, 16, 0, 0);
+#endif
+            }
+        };
+        float mvA[16], evA;
+        if (st0 < st1) {
+            stage_half(st0, false);
+            load_m(st0 * H3_TILE, mvA, evA);
+            stage_half(st0, true);
+        }
+        for (int st = st0; st < st1; ++st) {
+            float mv[16], ev;
+            f16x8 ph[2], pl[2];
+            __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): K and M of this tile landed (V may not have)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mv[r] = mvA[r];
+            ev = evA;
+            const bool more = st + 1 < st1;
+            qk_softmax(slot, st * H3_TILE, mv, ev, ph, pl, st == st0, [&] {
+                if (more) {
+                    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this tile's K reads returned
+                    stage_half(st + 1, false);
+                }
+            });
+            if (more)
+                __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): this tile's V landed (the next K may not have)
+            else
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            pv(slot + H3_KTB, ph, pl);
+            if (more) {
+                load_m((st + 1) * H3_TILE, mvA, evA);
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this tile's V reads returned
+                stage_half(st + 1, true);
+            }
+        }
+        l_run = halves_sum(l_run);
+        return;
+    }
     float mvA[16], evA;  // EARLY: the next tile's M, loaded a tile ahead
     if (st0 < st1) {
         stage(st0, 0);
@@ -640,27 +695,16 @@ PDSC_DEV void attention_h3_core(const _Float16 *__restrict__ Qs, const _Float16 
             // tile st0 + 1 went out before the loop; tile st + 1's slot held tile
             // st - 1, released by the barrier that ended iteration st - 1
             if (st > st0 && st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
-        } else if constexpr (WS > 0) {
-            // one slot per wave: tile st + 1 is staged after tile st's reads (below)
-            load_m(st * H3_TILE, mv, ev);
-            if (st > st0) sync();  // tile st landed (staged at the end of the previous iteration)
         } else {
             load_m(st * H3_TILE, mv, ev);  // (padding waves' reads stay inside the pair's M)
             if (st + 1 < st1) stage(st + 1, ((st + 1 - st0) % H3_NSLOT));
         }
         // padding waves (q0 >= Npad) compute on clamped operands and store nothing
-        qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl, st == st0);
+        qk_softmax(slot_base(st), st * H3_TILE, mv, ev, ph, pl, st == st0, [] {});
         ATT_STAMP(stp, si + 3);
         pv(slot_base(st) + H3_KTB, ph, pl);
         ATT_STAMP(stp, si + 4);
-        if constexpr (WS > 0) {
-            if (st + 1 < st1) {
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this tile's LDS reads returned
-                stage(st + 1, 0);
-            }
-        } else {
-            sync();
-        }
+        sync();
         ATT_STAMP(stp, si + 5);
     }
     l_run = halves_sum(l_run);
