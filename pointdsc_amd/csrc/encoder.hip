@@ -158,19 +158,25 @@ static int att_nw(int B, int N) {
     if (att_tiny(B, N)) return 1;
     return (long)B * ((N + QB - 1) / QB) <= 16 ? v : ATT_NW;
 }
-// The smallest batches (at most 8 query blocks of 128: a single pair to N =
-// 1024): 32-query workgroups whose key splits fill ONE round of
+// The smallest batches (at most 16 query blocks of 128 and splits of <= 24 key
+// tiles: a single pair to N = 1536, two to 1024, four to 512): 32-query workgroups whose key splits fill ONE round of
 // att_tiny_slots() (128) workgroups (a 1000-key pair: 32 blocks x 4 splits of 8
 // tiles, run by attention_h3_ws_kernel's 4 waves) instead of 16 blocks x 16
 // splits of 2 -- a quarter of the split partials, so pw_mid combines them
 // itself (use_precombine: fewer than 16 splits) and the combine_rows launch goes.
 // A/B knob PDSC_ATT_TINY=0 (measurement only).
+static int att_tiny_slots();
 static bool att_tiny(int B, int N) {
-    static const bool off = [] {
+    static const int lim = [] {  // PDSC_ATT_TINY=0: off; =n: up to n blocks of 128 queries (measurement only)
         const char *e = getenv("PDSC_ATT_TINY");
-        return e && e[0] == '0';
+        return e ? atoi(e) : 16;
     }();
-    return !off && (long)B * ((N + QB - 1) / QB) <= 8;
+    if ((long)B * ((N + QB - 1) / QB) > lim) return false;
+    // splits of at most 24 key tiles (6 per wave of the wave-split kernel): ms per
+    // forward, 8 -> 16-block limit (profiles/r06_ab_tiny16.log): 2 x 1000 0.431 ->
+    // 0.382, 4 x 500 0.374 -> 0.324, 1 x 1500 (24 tiles) 0.456 -> 0.439, but 1 x 2000
+    // (32 tiles) 0.489 -> 0.504, which keeps the two-wave split plan
+    return attention_h3_grid<1>(B, N, std::min(att_target(), att_tiny_slots())).sps <= 24;
 }
 // The tiny plan's waves per workgroup splitting each key split's tiles
 // (attention_h3_ws_kernel): 4 (default), 2, or 1 = the one-wave kernel.
