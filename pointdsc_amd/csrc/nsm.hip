@@ -257,12 +257,9 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
     // 256 i + 4 l + e (16-B loads); R = 0: re-read from memory.  More than
     // KNN_FASTCAP qualifying keys (heavy ties, adversarial orders) falls through
     // to the radix select below.
-    if (want <= 64) {
-        constexpr int NR = R > 0 ? R : 1;
-        uint32_t key[NR];
-        const int NI = R > 0 ? R : (N + 63) / 64;
-        // index of this lane's i-th key
-        auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
+    constexpr int NR = R > 0 ? R : 1;
+    uint32_t key[NR];  // R > 0: the row in registers (fast path and radix fallback)
+    {
         if constexpr (R > 0) {
             if ((Nstr & 3) == 0) {  // rows 16-B aligned (wave-uniform)
                 // buffer loads over the row's first round_up(N, 4) keys (lane offset
@@ -288,6 +285,11 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 }
             }
         }
+    }
+    if (want <= 64) {
+        const int NI = R > 0 ? R : (N + 63) / 64;
+        // index of this lane's i-th key
+        auto J = [&](int i) -> int { return R > 0 ? 256 * (i >> 2) + 4 * lane + (i & 3) : lane + 64 * i; };
         auto K = [&](int i) -> uint32_t {
             if constexpr (R > 0) {
                 return key[i];
@@ -386,9 +388,181 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
             return;
         }
     }
+    KNN_COUNT(2, 1);
+    if constexpr (R > 0) {
+        // Radix fallback on the row held in registers (r06: the memory form below
+        // re-reads the row from L2 in every histogram pass, one dependent load per
+        // atomic; the single N = 5000 pair's clustered rows took 90 us in it).
+        // Lane l holds keys 256 b + 4 l + e (block b = i / 4, e = i % 4, ~0u past N):
+        // counting passes do not care about order, and the collection pass ranks
+        // a block's keys in index order from its four ballots.  The same selection
+        // as the memory form, so the same kNN rows.
+        uint32_t kmin = 0xffffffffu, kmax = 0u;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const bool valid = 256 * (i >> 2) + 4 * lane + (i & 3) < N;
+            if (valid) {
+                kmin = min(kmin, key[i]);
+                kmax = max(kmax, key[i]);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        }
+        uint32_t *hb = hist[wave];
+        uint32_t need = want, prefix = kmin, mask = 0xffffffffu, bin_cnt = want;
+        bool small_bin = false;
+        if (kmin != kmax) {
+            const int top = 31 - __clz((int)(kmin ^ kmax));
+            mask = top == 31 ? 0u : ~((2u << top) - 1u);
+            prefix = kmin & mask;
+            for (int hi = top; hi >= 0; hi -= 8) {
+                const int lo = max(hi - 7, 0);
+                const uint32_t dm = (2u << (hi - lo)) - 1u;
+                KNN_COUNT(3, 1);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hb[lane + 64 * e] = 0;
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    const uint32_t u = key[i];
+                    if (256 * (i >> 2) + 4 * lane + (i & 3) < N && (u & mask) == prefix)
+                        atomicAdd(&hb[(u >> lo) & dm], 1u);
+                    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint32_t c[4], tot = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    c[e] = hb[4 * lane + e];
+                    tot += c[e];
+                }
+                uint32_t incl = tot;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (lane >= o) incl += y;
+                }
+                const uint32_t base = incl - tot;
+                uint32_t my_bin = 0, my_need = 0, my_cnt = 0;
+                const bool hit = base < need && need <= incl;
+                if (hit) {
+                    uint32_t cum = base;
+                    bool done = false;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (!done && cum + c[e] >= need) {
+                            my_bin = 4 * lane + e;
+                            my_need = need - cum;
+                            my_cnt = c[e];
+                            done = true;
+                        }
+                        cum += c[e];
+                    }
+                }
+                const int src_lane = __ffsll((unsigned long long)__ballot(hit)) - 1;
+                const uint32_t bin = __shfl(my_bin, src_lane);
+                const uint32_t cnt = __shfl(my_cnt, src_lane);
+                need = __shfl(my_need, src_lane);
+                prefix |= bin << lo;
+                mask |= dm << lo;
+                bin_cnt = cnt;
+                if (cnt == need) break;
+                if (cnt <= KNN_BINCAP) {
+                    small_bin = true;
+                    break;
+                }
+            }
+        }
+        const uint32_t nless = want - need;
+        const unsigned long long below = (1ull << lane) - 1ull;
+        uint32_t pl = 0, pe = 0;
+#pragma unroll
+        for (int i4 = 0; i4 < R / 4; ++i4) {
+            bool less[4], eq[4];
+            unsigned long long lm[4], em[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t u = key[4 * i4 + e], um = u & mask;
+                const bool valid = 256 * i4 + 4 * lane + e < N;
+                less[e] = valid && um < prefix;
+                eq[e] = valid && um == prefix;
+                lm[e] = __ballot(less[e]);
+                em[e] = __ballot(eq[e]);
+            }
+            // index-order rank inside the block: every key of the lanes below, then
+            // this lane's keys before e
+            uint32_t lb = 0, eb = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                lb += __popcll(lm[e] & below);
+                eb += __popcll(em[e] & below);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j = 256 * i4 + 4 * lane + e;
+                const uint32_t u = key[4 * i4 + e];
+                if (less[e]) {
+                    const uint32_t pos = pl + lb;
+                    if (pos < want) {
+                        ckey[wave][pos] = u;
+                        cidx[wave][pos] = j;
+                    }
+                }
+                if (eq[e]) {
+                    const uint32_t r = pe + eb;
+                    if (small_bin) {
+                        bkey[wave][r] = u;
+                        bidx[wave][r] = j;
+                    } else if (r < need) {
+                        ckey[wave][nless + r] = u;
+                        cidx[wave][nless + r] = j;
+                    }
+                }
+                lb += less[e];
+                eb += eq[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                pl += __popcll(lm[e]);
+                pe += __popcll(em[e]);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one block's ballots live at a time
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (small_bin) KNN_COUNT(4, 1);
+        if (small_bin) {
+            for (int e = lane; e < (int)bin_cnt; e += 64) {
+                const uint32_t ku = bkey[wave][e];
+                const int ki = bidx[wave][e];
+                uint32_t rank = 0;
+                for (int m = 0; m < (int)bin_cnt; ++m) {
+                    const uint32_t mu = bkey[wave][m];
+                    rank += (mu < ku) || (mu == ku && bidx[wave][m] < ki);
+                }
+                if (rank < need) {
+                    ckey[wave][nless + rank] = ku;
+                    cidx[wave][nless + rank] = ki;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (lane < (int)want) {
+            const uint32_t ku = ckey[wave][lane];
+            const int ki = cidx[wave][lane];
+            int rank = 0;
+            for (int m = 0; m < (int)want; ++m) {
+                const uint32_t mu = ckey[wave][m];
+                rank += (mu < ku) || (mu == ku && cidx[wave][m] < ki);
+            }
+            if (rank > 0) knn[((size_t)b * Sstr + s) * k + rank - 1] = ki;  // drop position 0 (:68)
+        }
+        return;
+    }
     // Radix fallback, keys re-read from memory (lane l owns keys l + 64 i, so a
     // ballot over lanes visits keys in index order).
-    KNN_COUNT(2, 1);
     const int NI = (N + 63) / 64;
     auto K = [&](int i) -> uint32_t {
         const int j = lane + 64 * i;
