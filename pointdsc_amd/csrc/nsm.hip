@@ -298,17 +298,30 @@ __global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict
                 return j < N ? row[j] : 0xffffffffu;
             }
         };
-        uint32_t lmin = 0xffffffffu;
+        // Long rows (R >= 32: N > 2048) also keep each lane's second-smallest key:
+        // the threshold then comes from 128 values, about half as many keys pass it
+        // (clustered rows of a trained network: fewer rows overflow the fast path
+        // into the radix select; r06).  Still at least `want` keys <= tau0 (a lane's
+        // two values are two of its keys), so the same rows result.
+        constexpr bool TWO = R >= 32;
+        uint32_t lmin = 0xffffffffu, lmin2 = 0xffffffffu;
 #pragma unroll
         for (int i = 0; i < NI; ++i)
-            if (R > 0 || J(i) < N) lmin = min(lmin, K(i));  // R > 0: keys past N are ~0u
-        // tau0 = the want-th smallest lane minimum: the smallest value v with
-        // #{lanes: lmin <= v} >= want, built bit by bit from the top (one
-        // compare + ballot + scalar popcount per bit instead of 64 readlanes)
+            if (R > 0 || J(i) < N) {  // R > 0: keys past N are ~0u
+                const uint32_t x = K(i);
+                if constexpr (TWO) lmin2 = min(lmin2, max(lmin, x));
+                lmin = min(lmin, x);
+            }
+        // tau0 = the want-th smallest lane minimum (TWO: of the 128 lane minima and
+        // second minima): the smallest value v with #{lanes: lmin <= v} (+ #{lanes:
+        // lmin2 <= v}) >= want, built bit by bit from the top (one compare + ballot
+        // + scalar popcount per bit instead of 64 readlanes)
         uint32_t tau0 = 0;
         for (int bit = 31; bit >= 0; --bit) {
             const uint32_t probe = tau0 | ((1u << bit) - 1u);  // this bit 0, all lower bits 1
-            if ((uint32_t)__popcll(__ballot(lmin <= probe)) < want) tau0 |= 1u << bit;
+            uint32_t cnt = (uint32_t)__popcll(__ballot(lmin <= probe));
+            if constexpr (TWO) cnt += (uint32_t)__popcll(__ballot(lmin2 <= probe));
+            if (cnt < want) tau0 |= 1u << bit;
         }
         const unsigned long long below = (1ull << lane) - 1ull;
         // the key indices recomputed from an opaque base: otherwise the compiler
