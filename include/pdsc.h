@@ -76,6 +76,18 @@ enum pdsc_precision {
  * marks: its conf output carries the NaN.                                    */
 int32_t pdsc_range_status(const void *forward_workspace, int32_t B, int32_t *flags, pdsc_stream_t stream);
 
+/* The same answer without the per-pair flags and without a copy: enqueues on
+ * `stream` a one-wavefront kernel that writes whether any of the B pairs is
+ * marked into a word of coherent page-locked host memory (one per host thread,
+ * allocated on first use), and spins on that word until the kernel has run --
+ * i.e. until everything enqueued on `stream` before it has completed -- then
+ * returns PDSC_OK or PDSC_ERR_RANGE.  After 20 ms of spinning it blocks in
+ * hipStreamSynchronize instead (a long queue; a faulted stream is reported as
+ * PDSC_ERR_HIP).  The bs = 1 drop-in path (pointdsc_amd.PointDSC.forward) uses
+ * it: the reference's forward returns with no host synchronisation at all
+ * (models/PointDSC.py:128-197); this one waits only for the guard's answer. */
+int32_t pdsc_range_poll(const void *forward_workspace, int32_t B, pdsc_stream_t stream);
+
 /* Hyper-parameters of PointDSC.__init__ (models/PointDSC.py:81-100). */
 typedef struct pdsc_config {
     int32_t in_dim;           /* 6 (1 .. 128; the reference's 6, 9, 12, 70) */

@@ -51,21 +51,6 @@ _nn_module.register_module_module_registration_hook(_bump_epoch)
 # workspaces up to this size stay cached per stream between forwards
 _WS_CACHE_LIMIT = 256 << 20
 
-_HIP = []
-
-
-def _hip():
-    """libamdhip64 (hipMemcpyAsync into the pinned range-flag word, hipStreamSynchronize)."""
-    if not _HIP:
-        h = ctypes.CDLL("libamdhip64.so")
-        h.hipMemcpyAsync.restype = ctypes.c_int
-        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
-        h.hipStreamSynchronize.restype = ctypes.c_int
-        h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
-        _HIP.append(h)
-    return _HIP[0]
-
-
 class NonLocalBlock(nn.Module):
     """Parameter holder with the reference's layout (models/PointDSC.py:9-25)."""
 
@@ -323,10 +308,10 @@ class PointDSC(nn.Module):
     def _forward_one(self, corr_pos, src, tgt):
         """The drop-in call's path (bs = 1, the reference drivers' shape): one C
         call on the current stream with the cached workspace, then the fp16 range
-        guard's flag read through a pinned host word (a 4-byte D2H into page-locked
-        memory + one stream synchronisation: 12.6 us idle on MI355X, against 23.6
-        us for pdsc_range_status's copy into pageable memory,
-        tools/dropin_breakdown.py).  Returns None -- the caller then takes the
+        guard's answer through pdsc_range_poll (a one-wavefront kernel stores it
+        into a coherent host word the host spins on: no D2H copy, no stream
+        synchronisation; tools/dropin_breakdown.py times the alternatives).
+        Returns None -- the caller then takes the
         general path, which raises the precise error or re-runs a marked pair in
         exact fp32 -- when the workspace is not cacheable or the pair is marked."""
         dev = src.device
@@ -338,37 +323,32 @@ class PointDSC(nn.Module):
         cfg, pk = self.pdsc_config(), self.packed_weights()
         kernels._check_inputs(cfg, corr_pos, src, tgt)
         N = src.shape[1]
-        sh = torch.cuda.current_stream(dev).cuda_stream
+        sh = torch._C._cuda_getCurrentRawStream(dev.index)  # = torch.cuda.current_stream(dev).cuda_stream
         cache = self.__dict__.setdefault("_one_cache", {})
         ent = cache.get((dev, sh, N, id(cfg)))
         if ent is None:
             ws = self._workspace(cfg, 1, N, dev)
             if ws is None:
                 return None
-            pins = self.__dict__.setdefault("_pinned", {})
-            pinned = pins.get((dev, sh))
-            if pinned is None:
-                pinned = pins[(dev, sh)] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             if len(cache) > 256:
                 cache.clear()
             L = _lib.load()
             ent = cache[(dev, sh, N, id(cfg))] = (
                 L.pdsc_forward_testing, ctypes.byref(cfg), L.pdsc_forward_workspace_bytes(ctypes.byref(cfg), 1, N),
-                self.__dict__["_ws_cache"], (dev, sh), pinned, pinned.numpy(), ctypes.c_void_p(sh), _hip())
-        fwd, cfgp, nb, wsc, wkey, pinned, pinned_np, sp, hip = ent
+                self.__dict__["_ws_cache"], (dev, sh), ctypes.c_void_p(sh), L.pdsc_range_poll)
+        fwd, cfgp, nb, wsc, wkey, sp, poll = ent
         ws = wsc.get(wkey)
         if ws is None or ws.numel() < nb:  # another model size / N grew the stream's workspace meanwhile
             ws = self._workspace(cfg, 1, N, dev)
         out = torch.empty(16 + N, dtype=torch.float32, device=dev)  # one allocation, two views
-        trans, labels = out[:16].view(1, 4, 4), out[16:].view(1, N)
+        trans, labels = out.as_strided((1, 4, 4), (16, 4, 1)), out.as_strided((1, N), (N, 1), 16)
         wp = ws.data_ptr()
         _lib.check(fwd(cfgp, pk.data_ptr(), corr_pos.data_ptr(), src.data_ptr(), tgt.data_ptr(), 1, N,
                        trans.data_ptr(), labels.data_ptr(), None, None, wp, nb, sp), "pdsc_forward_testing")
-        # the range flag: the forward workspace's first int32 (include/pdsc.h, pdsc_range_status)
-        if hip.hipMemcpyAsync(pinned_np.ctypes.data, ctypes.c_void_p(wp), 4, 2, sp) != 0 \
-                or hip.hipStreamSynchronize(sp) != 0:
-            return None  # the general path reports it through pdsc_range_status
-        if pinned_np[0] != 0:  # marked by the range guard: the general path re-runs it in exact fp32
+        # the range guard's answer through pdsc_range_poll's host word (include/pdsc.h):
+        # PDSC_ERR_RANGE (marked) -> the general path re-runs the pair in exact fp32;
+        # any other error -> the general path reports it precisely
+        if poll(ctypes.c_void_p(wp), 1, sp) != 0:
             return None
         return {"final_trans": trans, "final_labels": labels, "M": None}
 

@@ -114,6 +114,7 @@ _PROTOS = {
     "pdsc_compute_fpfh": (c_int32, [vp, vp, c_int32, c_float, c_int32, vp, vp, vp, c_size_t, vp]),
     "pdsc_forward_training_workspace_bytes": (c_size_t, [CFG, c_int32, c_int32]),
     "pdsc_range_status": (c_int32, [vp, c_int32, ctypes.POINTER(c_int32), vp]),
+    "pdsc_range_poll": (c_int32, [vp, c_int32, vp]),
     "pdsc_forward_training": (c_int32, [CFG, vp, vp, vp, vp, c_int32, c_int32, vp, vp, vp, vp, vp, c_size_t, vp]),
     "pdsc_spectral_matching_loss_workspace_bytes": (c_size_t, [c_int32, c_int32]),
     "pdsc_spectral_matching_loss": (c_int32, [vp, vp, c_int32, c_int32, c_int32, vp, vp, c_size_t, vp]),

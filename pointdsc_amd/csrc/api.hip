@@ -3,6 +3,7 @@
 // Host-side orchestration only: argument checks, workspace carving and kernel
 // launches on the caller's stream.  No allocation, no synchronisation.
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1051,6 +1052,73 @@ int32_t pdsc_range_status(const void *ws, int32_t B, int32_t *flags, pdsc_stream
         bad += h[b] != 0;
     }
     if (bad) return fail(PDSC_ERR_RANGE, "%d of %d pairs left the fp16 range (rerun them with PDSC_PRECISION_F32)", bad, B);
+    return PDSC_OK;
+}
+
+// pdsc_range_poll: one wavefront ORs the B marks and stores (seq << 1) | any into
+// a word of coherent page-locked host memory (a system-scope release store);
+// the host spins on the word instead of a D2H copy + stream synchronisation
+// (the copy alone: 12.6 us on an idle MI355X stream, tools/dropin_breakdown.py).
+__global__ __launch_bounds__(64) void range_publish_kernel(const int32_t *__restrict__ range, int B,
+                                                           uint32_t *word, uint32_t seq) {
+    bool any = false;
+    for (int b = threadIdx.x; b < B; b += 64) any |= range[b] != 0;
+    const bool m = __ballot(any) != 0;
+    if (threadIdx.x == 0) __hip_atomic_store(word, (seq << 1) | (m ? 1u : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+namespace {
+struct PollWord {
+    uint32_t *host = nullptr, *dev = nullptr;
+    uint32_t seq = 0;
+    ~PollWord() {
+        if (host) (void)hipHostFree(host);
+    }
+};
+thread_local PollWord g_poll;  // one word per host thread: its calls wait one at a time
+}  // namespace
+
+int32_t pdsc_range_poll(const void *ws, int32_t B, pdsc_stream_t stream) {
+    if (!ws || B < 1) return fail(PDSC_ERR_ARG, "ws=%p B=%d", ws, B);
+    hipStream_t s = S_(stream);
+    PollWord &w = g_poll;
+    if (!w.host) {
+        void *h = nullptr, *dp = nullptr;
+        HIPCHK(hipHostMalloc(&h, 64, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+        if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) {
+            (void)hipHostFree(h);
+            return fail(PDSC_ERR_HIP, "hipHostGetDevicePointer");
+        }
+        w.host = static_cast<uint32_t *>(h);
+        w.dev = static_cast<uint32_t *>(dp);
+        __atomic_store_n(w.host, 0u, __ATOMIC_RELEASE);
+    }
+    w.seq = (w.seq + 1) & 0x7fffffffu;
+    if (w.seq == 0) w.seq = 1;  // 0 is the word's initial value
+    const uint32_t seq = w.seq;
+    hipLaunchKernelGGL(range_publish_kernel, dim3(1), dim3(64), 0, s, static_cast<const int32_t *>(ws), (int)B, w.dev,
+                       seq);
+    HIPCHK(hipGetLastError());
+    // spin ~20 ms at most (the forward's own device time is well below), then
+    // block in hipStreamSynchronize: it also reports a faulted stream
+    uint32_t v = 0;
+    bool seen = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+        v = __atomic_load_n(w.host, __ATOMIC_ACQUIRE);
+        if ((v >> 1) == seq) {
+            seen = true;
+            break;
+        }
+        __builtin_ia32_pause();
+        if ((it & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (!seen) {
+        HIPCHK(hipStreamSynchronize(s));
+        v = __atomic_load_n(w.host, __ATOMIC_ACQUIRE);
+        if ((v >> 1) != seq) return fail(PDSC_ERR_HIP, "range word %u after the stream drained (expected %u)", v >> 1, seq);
+    }
+    if (v & 1u) return fail(PDSC_ERR_RANGE, "a pair of %d left the fp16 range (rerun it with PDSC_PRECISION_F32)", B);
     return PDSC_OK;
 }
 

@@ -212,6 +212,9 @@ hipError_t launch_split_rows(const float *x, size_t rows, _Float16 *out, hipStre
 // pick the `need` smallest -- usually after ONE histogram pass) or its first
 // `need` keys in index order; the k+1 candidates are ranked by (key, index)
 // and the first is dropped positionally (models/common.py:68).
+// Rows to R = 80 keep 4 waves per SIMD (<= 128 VGPRs; the register fallback
+// alone would take 142 at R = 80, and 8 x 5000's 4000 row waves would need two
+// rounds of 3: r06, profiles/r06_ab_knn_wpe.log).
 constexpr int KNN_BINCAP = 64;
 constexpr int KNN_FASTCAP = 128;
 
@@ -233,7 +236,7 @@ extern "C" int pdsc_diag_knn_paths(unsigned *host, int reset) {
 #endif
 
 template <int R>
-__global__ __launch_bounds__(256) void knn_select_kernel(const float *__restrict__ dist, int Nstr, int Sstr,
+__global__ __launch_bounds__(256, R <= 80 ? 4 : 1) void knn_select_kernel(const float *__restrict__ dist, int Nstr, int Sstr,
                                                          int k, int *__restrict__ knn, Ragged rg, int bitonic) {
     __shared__ uint32_t hist[4][256];
     __shared__ uint32_t ckey[4][64];

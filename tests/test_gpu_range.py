@@ -66,9 +66,18 @@ def test_range_marks_and_poisons(gpu_device):
     flags = (ctypes.c_int32 * 4)()
     assert L_.pdsc_range_status(kernels._p(plan.ws), 4, flags, kernels._stream(gpu_device)) == kernels.PDSC_ERR_RANGE
     assert list(flags) == [0, 0, 1, 0]
+    # pdsc_range_poll: the same answer through the host word, repeatedly (the sequence advances)
+    for _ in range(3):
+        assert L_.pdsc_range_poll(kernels._p(plan.ws), 4, kernels._stream(gpu_device)) == kernels.PDSC_ERR_RANGE
+    assert L_.pdsc_range_poll(kernels._p(plan.ws), 2, kernels._stream(gpu_device)) == 0  # pairs 0-1 unmarked
     plan.run(corr0, src, tgt)
+    assert L_.pdsc_range_poll(kernels._p(plan.ws), 4, kernels._stream(gpu_device)) == 0
     assert L_.pdsc_range_status(kernels._p(plan.ws), 4, flags, kernels._stream(gpu_device)) == 0
     assert list(flags) == [0, 0, 0, 0]
+    # the poll returns once the stream's earlier work has run: the outputs are final
+    plan.run(corr, src, tgt)
+    assert L_.pdsc_range_poll(kernels._p(plan.ws), 4, kernels._stream(gpu_device)) == kernels.PDSC_ERR_RANGE
+    assert torch.isnan(plan.trans[2]).all() and torch.isfinite(plan.trans[0]).all()
 
 
 def test_module_reruns_marked_pairs_in_f32(gpu_device):

@@ -74,6 +74,10 @@ def main():
         stream.synchronize()
         return int(pinned[0])
 
+    def raw_poll():
+        L.pdsc_forward_testing(*args)
+        return L.pdsc_range_poll(ctypes.c_void_p(ws.data_ptr()), 1, sp)
+
     def wrap():
         kernels.forward_testing(cfg, pk, c, s, t, ws=ws, check_range=False)
 
@@ -90,12 +94,14 @@ def main():
     out["raw_sync_each_us"] = wall(raw_sync)
     out["raw_range_status_us"] = wall(raw_rs)
     out["raw_pinned_copy_us"] = wall(raw_pinned)
+    out["raw_poll_us"] = wall(raw_poll)
     out["wrapper_async_us"] = wall(wrap)
     out["dropin_us"] = wall(lambda: m(data))
     # host-only pieces (GPU idle)
     torch.cuda.synchronize()
     out["range_status_idle_us"] = wall(lambda: kernels.range_flags(ws, 1, dev))
     out["pinned_copy_idle_us"] = wall(lambda: (pinned.copy_(flags, non_blocking=True), stream.synchronize()))
+    out["poll_idle_us"] = wall(lambda: L.pdsc_range_poll(ctypes.c_void_p(ws.data_ptr()), 1, sp))
     out["stream_sync_idle_us"] = wall(lambda: hip.hipStreamSynchronize(sp))
     out["current_stream_us"] = wall(lambda: torch.cuda.current_stream(dev), 2000)
     out["empty_4x4_us"] = wall(lambda: torch.empty((1, 4, 4), dtype=torch.float32, device=dev), 2000)
