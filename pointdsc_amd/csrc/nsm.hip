@@ -1170,6 +1170,34 @@ constexpr int HS = 8;     // seeds per count_inliers workgroup
 
 PDSC_DEV void kabsch_finish(const float H[9], const float cA[3], const float cB[3], float *T);
 
+// for (n = tid; n < N; n += NT) body(n, src row n, tgt row n) with RU rows'
+// loads issued together: the pair's rows come from L2, and a loop that loads
+// and consumes one row per trip waits a full round trip per row (r06 stamps of
+// best_refine at N = 5000: 6.7 us per pass of 20 rows per thread).  body runs
+// in the same n order, so sums accumulate in the same order: the same bits.
+// A/B build knob: -DROWS_RU=1 consumes each row as it is loaded (measurement only)
+#ifndef ROWS_RU
+#define ROWS_RU 8
+#endif
+template <int NT, int RU = ROWS_RU, typename F>
+PDSC_DEV void for_rows(const float *__restrict__ sb, const float *__restrict__ tb, int N, int tid, F body) {
+    for (int n0 = tid; n0 < N; n0 += RU * NT) {
+        float a[RU][3], c[RU][3];
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int n = min(n0 + u * NT, N - 1);  // (clamped: an in-range row, not consumed)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                a[u][e] = sb[3 * n + e];
+                c[u][e] = tb[3 * n + e];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u)
+            if (n0 + u * NT < N) body(n0 + u * NT, a[u], c[u]);
+    }
+}
+
 // SOLVE (small batches, kabsch_small): lane 0 of the seed's wave also finishes
 // the Kabsch solve (kabsch_finish on the same 15 sums kabsch_solve_kernel would
 // read back: the same bits) and writes trans -- one launch instead of two.
@@ -1242,9 +1270,9 @@ __global__ __launch_bounds__(256) void kabsch_sums_kernel(const float *__restric
             for (int e = 0; e < 12; ++e) Tb[e] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, T[e])));
             const int n = rg.n(b, N);
             int c = 0;
-            for (int j = lane; j < n; j += 64)
-                c += residual_sq(Tb, sb[3 * j], sb[3 * j + 1], sb[3 * j + 2], tb[3 * j], tb[3 * j + 1], tb[3 * j + 2]) <
-                     tau2;  // L2 < tau (:327-328)
+            for_rows<64>(sb, tb, n, lane, [&](int, const float (&p)[3], const float (&q)[3]) {
+                c += residual_sq(Tb, p[0], p[1], p[2], q[0], q[1], q[2]) < tau2;  // L2 < tau (:327-328)
+            });
             c = wave_sum(c);
             if (lane == 0) counts[(size_t)b * S + s] = c;
         }
@@ -1395,7 +1423,14 @@ PDSC_DEV bool select_best_wg(const float *__restrict__ src, const float *__restr
         // fp16's range in a 3xfp16 contraction turns into NaN (inf hi, -inf lo),
         // which the encoder's NaN-propagating ReLUs carry into every logit
         int bad = 0;
-        for (int n = tid; n < N; n += 256) bad |= !__builtin_isfinite(conf[(size_t)b * Nstr + n]);
+        const float *cb = conf + (size_t)b * Nstr;
+        for (int n0 = tid; n0 < N; n0 += 8 * 256) {  // 8 loads in flight per thread
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = cb[min(n0 + 256 * u, N - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bad |= !__builtin_isfinite(v[u]);
+        }
         bad = __syncthreads_or(bad);
         if (range && tid == 0) range[b] = bad;
         if (bad) {
@@ -1435,11 +1470,10 @@ PDSC_DEV bool select_best_wg(const float *__restrict__ src, const float *__restr
 #pragma unroll
     for (int e = 0; e < 12; ++e) T[e] = Ts[e];
     const float *sb = src + (size_t)b * Nstr * 3, *tb = tgt + (size_t)b * Nstr * 3;
-    for (int n = tid; n < N; n += 256) {
-        const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
-                                  tb[3 * n + 2]);
+    for_rows<256>(sb, tb, N, tid, [&](int n, const float (&a)[3], const float (&c)[3]) {
+        const float L2 = residual(T, a[0], a[1], a[2], c[0], c[1], c[2]);
         labels[(size_t)b * Nstr + n] = (L2 < tau) ? 1.0f : 0.0f;
-    }
+    });
     for (int n = N + tid; n < Nstr; n += 256) labels[(size_t)b * Nstr + n] = 0.0f;  // a ragged pair's padding
     return true;
 }
@@ -1539,6 +1573,21 @@ PDSC_DEV void block_rigid_h(const float *__restrict__ A, const float *__restrict
 }
 
 // ---------------------------------------------------- a11 post-refinement
+// Diagnostic build only (-DATT_STAMPS, tools/refine_stamps.py): pair 0's
+// workgroup stamps s_memrealtime into the stamp buffer's last wave slot at the
+// refinement's phase ends (BR_ST(i): 0 start, 1 select done, 2 + 3 it + {0, 1,
+// 2}: iteration it's count pass, H pass, solve; 98 the iterations run, 99 end).
+#ifdef ATT_STAMPS
+#define BR_ST(i)                                                                                         \
+    do {                                                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && (i) < ST_PER_WAVE)                                   \
+            g_att_stamps[(ST_WGS * 4 - 1) * ST_PER_WAVE + (i)] = __builtin_amdgcn_s_memrealtime();        \
+    } while (0)
+#else
+#define BR_ST(i) \
+    do {         \
+    } while (0)
+#endif
 // The refinement of pair blockIdx.x from the pose in Ts (LDS, every thread's
 // view current), written to trans[b] at the end.
 PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *__restrict__ src,
@@ -1551,9 +1600,8 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
         float T[12];
 #pragma unroll
         for (int e = 0; e < 12; ++e) T[e] = Ts[e];
-        auto wfun = [&](int n) -> float {
-            const float L2 = residual(T, sb[3 * n], sb[3 * n + 1], sb[3 * n + 2], tb[3 * n], tb[3 * n + 1],
-                                      tb[3 * n + 2]);
+        auto weight = [&](const float (&pa)[3], const float (&pb)[3]) -> float {
+            const float L2 = residual(T, pa[0], pa[1], pa[2], pb[0], pb[1], pb[2]);
             if (!(L2 < thr)) return 0.0f;
             const float r = L2 / thr;
             return 1.0f / (1.0f + r * r);  // 1/(1 + (L2/thr)^2) (:435)
@@ -1561,9 +1609,9 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
         // one pass: the inlier count (:423-426) and block_rigid's weighted sums of
         // the same T (the next iterate's weights), in block_rigid's order
         float c8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int n = tid; n < N; n += RB) {
-            const float ax = sb[3 * n], ay = sb[3 * n + 1], az = sb[3 * n + 2];
-            const float bx = tb[3 * n], by = tb[3 * n + 1], bz = tb[3 * n + 2];
+        for_rows<RB>(sb, tb, N, tid, [&](int, const float (&pa)[3], const float (&pb)[3]) {
+            const float ax = pa[0], ay = pa[1], az = pa[2];
+            const float bx = pb[0], by = pb[1], bz = pb[2];
             const float L2 = residual(T, ax, ay, az, bx, by, bz);
             float w = 0.0f;
             if (L2 < thr) {
@@ -1578,18 +1626,43 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
             c8[4] += bx * w;
             c8[5] += by * w;
             c8[6] += bz * w;
-        }
+        });
         block_sum<8>(c8, reinterpret_cast<float (*)[8]>(red), tid);
+        BR_ST(2 + 3 * it);
+#ifdef ATT_STAMPS
+        if (blockIdx.x == 0 && tid == 0) g_att_stamps[(ST_WGS * 4 - 1) * ST_PER_WAVE + 98] = it + 1;
+#endif
         const int cnt = (int)c8[7];
         if (cnt == prev) break;  // abs(int(inlier_num - previous_inlier_num)) < 1 (:426)
         prev = cnt;
         const float s7[7] = {c8[0], c8[1], c8[2], c8[3], c8[4], c8[5], c8[6]};
         float Tn[16];
-        block_rigid_h(sb, tb, N, wfun, s7, Tn, red, tid);
+        {   // block_rigid_h(sb, tb, N, wfun, s7, Tn, red, tid) with the rows loaded RU at a time
+            const float den = s7[0] + 1e-6f;
+            const float cA[3] = {s7[1] / den, s7[2] / den, s7[3] / den};
+            const float cB[3] = {s7[4] / den, s7[5] / den, s7[6] / den};
+            float H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for_rows<RB>(sb, tb, N, tid, [&](int, const float (&pa)[3], const float (&pb)[3]) {
+                const float w = weight(pa, pb);
+                if (w == 0.0f) return;
+                const float am[3] = {pa[0] - cA[0], pa[1] - cA[1], pa[2] - cA[2]};
+                const float bm[3] = {pb[0] - cB[0], pb[1] - cB[1], pb[2] - cB[2]};
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) H[3 * r + c] += (am[r] * w) * bm[c];
+            });
+            block_sum<9>(H, red, tid);
+            BR_ST(3 + 3 * it);
+            if (tid == 0) kabsch_finish(H, cA, cB, Tn);
+            __syncthreads();
+        }
         if (tid == 0)
             for (int e = 0; e < 16; ++e) Ts[e] = Tn[e];
         __syncthreads();
+        BR_ST(4 + 3 * it);
     }
+    BR_ST(99);
     if (tid < 16) trans[(size_t)b * 16 + tid] = Ts[tid];
 }
 
@@ -1618,9 +1691,11 @@ __global__ __launch_bounds__(RB) void best_refine_kernel(const float *__restrict
     __shared__ int wbest[4], wcnt[4];
     __shared__ float Ts[16];
     __shared__ float red[RW][9];
+    BR_ST(0);
     if (!select_best_wg(src, tgt, seed_trans, counts, Nstr, Sstr, tau, nullptr, nullptr, trans, labels, rg, conf, range,
                         wbest, wcnt, Ts))
         return;  // (workgroup-uniform) the range guard's NaN pose stays
+    BR_ST(1);
     post_refine_wg(Ts, trans, src, tgt, Nstr, thr, rg, red);
 }
 
