@@ -1602,9 +1602,9 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
         for (int e = 0; e < 12; ++e) T[e] = Ts[e];
         auto weight = [&](const float (&pa)[3], const float (&pb)[3]) -> float {
             const float L2 = residual(T, pa[0], pa[1], pa[2], pb[0], pb[1], pb[2]);
-            if (!(L2 < thr)) return 0.0f;
             const float r = L2 / thr;
-            return 1.0f / (1.0f + r * r);  // 1/(1 + (L2/thr)^2) (:435)
+            const float wv = 1.0f / (1.0f + r * r);  // 1/(1 + (L2/thr)^2) (:435)
+            return L2 < thr ? wv : 0.0f;
         };
         // one pass: the inlier count (:423-426) and block_rigid's weighted sums of
         // the same T (the next iterate's weights), in block_rigid's order
@@ -1613,12 +1613,13 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
             const float ax = pa[0], ay = pa[1], az = pa[2];
             const float bx = pb[0], by = pb[1], bz = pb[2];
             const float L2 = residual(T, ax, ay, az, bx, by, bz);
-            float w = 0.0f;
-            if (L2 < thr) {
-                const float r = L2 / thr;
-                w = 1.0f / (1.0f + r * r);
-                c8[7] += 1.0f;
-            }
+            // branch-free (the weight evaluated for every row, kept where L2 < thr):
+            // the rows of a trip are independent chains the scheduler interleaves
+            const bool in = L2 < thr;
+            const float r = L2 / thr;
+            const float wv = 1.0f / (1.0f + r * r);
+            const float w = in ? wv : 0.0f;
+            c8[7] += in ? 1.0f : 0.0f;
             c8[0] += w;
             c8[1] += ax * w;
             c8[2] += ay * w;
@@ -1643,8 +1644,9 @@ PDSC_DEV void post_refine_wg(float *Ts, float *__restrict__ trans, const float *
             const float cB[3] = {s7[4] / den, s7[5] / den, s7[6] / den};
             float H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for_rows<RB>(sb, tb, N, tid, [&](int, const float (&pa)[3], const float (&pb)[3]) {
+                // a zero weight adds (am 0) bm = +-0 to H, which leaves it as skipping the
+                // row did (H starts at +0 and x + -0 = x, +0 + -0 = +0): branch-free
                 const float w = weight(pa, pb);
-                if (w == 0.0f) return;
                 const float am[3] = {pa[0] - cA[0], pa[1] - cA[1], pa[2] - cA[2]};
                 const float bm[3] = {pb[0] - cB[0], pb[1] - cB[1], pb[2] - cB[2]};
 #pragma unroll
