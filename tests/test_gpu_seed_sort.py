@@ -1,4 +1,6 @@
-"""The other forms of a5 give exactly the compare kernels' bits: the opt-in
+"""The other forms of a5 give exactly the compare kernels' bits: the 2- and
+4-rows-per-thread NMS compare (local_max_rows_kernel, 2 the default for
+batches from r06; PDSC_LM_RPT=1 for the one-row local_max_kernel), the opt-in
 sorted forms (seeds.hip: bitonic-sorted NMS window and seed ranking, knob
 PDSC_SEED_SORT=1, measurement only) and the default select form of the ranking
 (radix-selected threshold + candidate ranking, seed_select_kernel; knob
@@ -19,7 +21,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 CASES = [(3, 1000, 100, 0.1), (2, 5000, 500, 0.1), (1, 777, 77, 0.6), (4, 64, 6, 0.05), (1, 6000, 600, 1e-3),
-         (2, 3000, 300, 0.02), (1, 9000, 4000, 0.02), (2, 2000, 1999, 0.0)]
+         (2, 3000, 300, 0.02), (1, 9000, 4000, 0.02), (2, 2000, 1999, 0.0),
+         (130, 640, 64, 0.08)]  # (the last: >= 1024 row blocks of 64 -> the 64-row NMS kernels)
 
 
 def _inputs(B, N, seed):
@@ -47,14 +50,17 @@ def _dump(path):
 def test_seed_kernel_forms_bit_identical(gpu_device, tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for tag, env in (("full", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="0")), ("sort", dict(PDSC_SEED_SORT="1")),
-                     ("select", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="1"))):
+    for tag, env in (("full", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="0", PDSC_LM_RPT="1")),
+                     ("sort", dict(PDSC_SEED_SORT="1")),
+                     ("select", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="1")),
+                     ("rows2", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="0", PDSC_LM_RPT="2")),
+                     ("rows4", dict(PDSC_SEED_SORT="0", PDSC_SEED_SELECT="0", PDSC_LM_RPT="4"))):
         path = tmp_path / f"seeds_{tag}.npz"
         code = f"import sys; sys.path[:0] = [{here!r}, {os.path.dirname(here)!r}]; " \
                f"import test_gpu_seed_sort as t; t._dump({str(path)!r})"
         subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), check=True, timeout=240)
         res[tag] = np.load(path)
-    for form in ("sort", "select"):
+    for form in ("sort", "select", "rows2", "rows4"):
         for k in res["full"].files:
             assert np.array_equal(res["full"][k], res[form][k]), (form, k)
 
