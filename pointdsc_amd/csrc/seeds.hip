@@ -566,17 +566,19 @@ static bool seed_sort_on() {
 }
 static size_t sort_lds(int N) { return (size_t)std::max(64, 1 << (32 - __builtin_clz((unsigned)std::max(N - 1, 1)))) * 8; }
 
-// rows per thread of the NMS compare kernel: 2 (local_max_rows_kernel) for
-// batches, 1 (local_max_kernel) for a single pair (r06: 8 x 5000 forward -15 /
-// -24 us on two boxes, 128 x 1000 within the spread, one pair +2 us at N = 1000
-// and +5-10 us at N = 5000: profiles/r06_ab_lm_batch.log, r06_ab_lm2.log); A/B
-// knob PDSC_LM_RPT=1|2|4 at every batch size (measurement only, the same bits)
-static int lm_rpt(int B) {
+// rows per thread of the NMS compare kernel: 2 (local_max_rows_kernel<16, 2>)
+// for batches on the 16-row blocks, else 1 (local_max_kernel) (r06: 8 x 5000
+// forward -15 / -24 us on two boxes and local_max 70.8 -> 60.3 us, but the
+// 64-row blocks slower with two rows -- 128 x 1000 31.4 -> 37.2 us, the ragged
+// bench 52 -> 72 us, r06j vs r06k profiles -- and one pair +2 us at N = 1000,
+// +5-10 us at N = 5000: profiles/r06_ab_lm*.log); A/B knob PDSC_LM_RPT=1|2|4
+// at every batch size (measurement only, the same bits)
+static int lm_rpt(int B, int N) {
     static const int r = [] {
         const char *e = getenv("PDSC_LM_RPT");
         return e ? atoi(e) : 0;
     }();
-    return r ? r : (B > 1 ? 2 : 1);
+    return r ? r : (B > 1 && seed_small(B, N) ? 2 : 1);
 }
 
 hipError_t launch_local_max(const float *src, const float *conf, int B, int N, float radius,
@@ -585,14 +587,14 @@ hipError_t launch_local_max(const float *src, const float *conf, int B, int N, f
         const size_t lds = sort_lds(N) + (size_t)N * sizeof(f32x4);
         hipLaunchKernelGGL(local_max_sort_kernel, dim3((N + SORT_NT - 1) / SORT_NT, B), dim3(SORT_NT), lds, s, src, conf,
                            N, sqrt_ge_threshold(radius), lm, rg);
-    } else if (lm_rpt(B) == 4) {
+    } else if (lm_rpt(B, N) == 4) {
         if (seed_small(B, N))
             hipLaunchKernelGGL((local_max_rows_kernel<16, 4>), dim3((N + 63) / 64, B), dim3(256), 0, s, src, conf, N,
                                sqrt_ge_threshold(radius), lm, rg);
         else
             hipLaunchKernelGGL((local_max_rows_kernel<64, 4>), dim3((N + 255) / 256, B), dim3(256), 0, s, src, conf,
                                N, sqrt_ge_threshold(radius), lm, rg);
-    } else if (lm_rpt(B) == 2) {
+    } else if (lm_rpt(B, N) == 2) {
         if (seed_small(B, N))
             hipLaunchKernelGGL((local_max_rows_kernel<16, 2>), dim3((N + 31) / 32, B), dim3(256), 0, s, src, conf, N,
                                sqrt_ge_threshold(radius), lm, rg);
