@@ -80,6 +80,34 @@ def test_range_marks_and_poisons(gpu_device):
     assert torch.isnan(plan.trans[2]).all() and torch.isfinite(plan.trans[0]).all()
 
 
+def test_range_poll_behind_a_long_queue(gpu_device):
+    """pdsc_range_poll when the stream holds more than its 20 ms spin (a GPU
+    sleep enqueued ahead of the forward): it falls back to hipStreamSynchronize
+    and still returns the forward's own answer, with the outputs final."""
+    from pointdsc_amd import _lib, kernels
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device)
+    corr0, _, _ = _batch(gpu_device, bad=())
+    L_ = _lib.load()
+    plan = kernels.ForwardPlan(m.pdsc_config(), m.packed_weights(), 4, 1000, gpu_device)
+    s = kernels._stream(gpu_device)
+    import time
+    plan.run(corr0, src, tgt)
+    torch.cuda.synchronize()
+    t_sleep = time.perf_counter()
+    torch.cuda._sleep(int(1e8))  # >= 50 ms of GPU spin (1e8 clocks) ahead of the forward
+    torch.cuda.synchronize()
+    t_sleep = time.perf_counter() - t_sleep
+    assert t_sleep > 0.03, t_sleep  # (else the case would not reach the fallback)
+    for c, want in ((corr, kernels.PDSC_ERR_RANGE), (corr0, 0)):
+        t0 = time.perf_counter()
+        torch.cuda._sleep(int(1e8))
+        plan.run(c, src, tgt)
+        assert L_.pdsc_range_poll(kernels._p(plan.ws), 4, s) == want
+        assert time.perf_counter() - t0 >= 0.9 * t_sleep  # it waited for the queue
+    assert torch.isfinite(plan.trans).all()
+
+
 def test_module_reruns_marked_pairs_in_f32(gpu_device):
     m, m32 = _model(gpu_device, "h3"), _model(gpu_device, "f32")
     corr, src, tgt = _batch(gpu_device)
