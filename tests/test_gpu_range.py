@@ -108,6 +108,43 @@ def test_range_poll_behind_a_long_queue(gpu_device):
     assert torch.isfinite(plan.trans).all()
 
 
+def test_range_poll_two_threads(gpu_device):
+    """pdsc_range_poll's host word is per host thread: two threads, each on its
+    own stream and plan (one batch marked, one not), polling concurrently, each
+    get their own forward's answer every time."""
+    import threading
+    from pointdsc_amd import _lib, kernels
+    m = _model(gpu_device, "h3")
+    corr, src, tgt = _batch(gpu_device)
+    corr0, _, _ = _batch(gpu_device, bad=())
+    L_ = _lib.load()
+    cfg, pk = m.pdsc_config(), m.packed_weights()
+    errors = []
+
+    def worker(c, want):
+        try:
+            st = torch.cuda.Stream(gpu_device)
+            with torch.cuda.stream(st):
+                plan = kernels.ForwardPlan(cfg, pk, 4, 1000, gpu_device)
+                for _ in range(8):
+                    plan.run(c, src, tgt)
+                    rc = L_.pdsc_range_poll(kernels._p(plan.ws), 4, ctypes.c_void_p(st.cuda_stream))
+                    if rc != want:
+                        errors.append((want, rc))
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    torch.cuda.synchronize()
+    ts = [threading.Thread(target=worker, args=(corr, kernels.PDSC_ERR_RANGE)),
+          threading.Thread(target=worker, args=(corr0, 0))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert errors == []
+
+
 def test_module_reruns_marked_pairs_in_f32(gpu_device):
     m, m32 = _model(gpu_device, "h3"), _model(gpu_device, "f32")
     corr, src, tgt = _batch(gpu_device)
